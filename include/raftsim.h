@@ -1,0 +1,168 @@
+/* raftsim.h — C ABI of libraftsim.so, the MI355X batched Raft simulator.
+ *
+ * The reference (angelini/raft-simulation) has no FFI; its seams are the handler loop and the
+ * three side-effect functions it calls. Each entry point below says which reference interface it
+ * replaces. Semantics: SIM_SPEC.md. Conventions: 0 on success, a negative errno on failure
+ * (-EINVAL bad argument, -ENOMEM allocation, -EIO HIP error); nothing throws across the ABI;
+ * output buffers are caller-allocated; the library owns device memory; a handle is used by one
+ * host thread at a time. `raft_sim_last_error()` explains the last failure (thread-local).
+ */
+#ifndef RAFTSIM_H
+#define RAFTSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAFT_SIM_ABI_VERSION 1
+#define RAFT_MAX_NODES 9
+#define RAFT_MAX_INBOX 16
+
+/* :state values of the node map (core.clj:33,70,76,81,87); 3 is the `:follwer` typo of
+ * candidate->follower (core.clj:76), a distinct fourth value. */
+enum raft_role { RAFT_FOLLOWER = 0, RAFT_CANDIDATE = 1, RAFT_LEADER = 2, RAFT_FOLLWER = 3 };
+
+/* :type values (server.clj:8-12 for requests, core.clj:95,109 for replies). */
+enum raft_msg_type {
+  RAFT_MSG_REQUEST_VOTE = 1,
+  RAFT_MSG_APPEND_ENTRIES = 2,
+  RAFT_MSG_CLIENT_SET = 3,
+  RAFT_MSG_VOTE_RESPONSE = 4,
+  RAFT_MSG_APPEND_RESPONSE = 5
+};
+
+/* Exceptions that end a node's `loop` (core.clj:202-203), SIM_SPEC D8. */
+enum raft_fault {
+  RAFT_RUNNING = 0,
+  RAFT_FAULT_IOOBE = 1,    /* nth past the end: val-at log.clj:23 */
+  RAFT_FAULT_NPE = 2,      /* (dec nil): core.clj:146 */
+  RAFT_FAULT_CCE = 3,      /* subvec of a LazySeq: log.clj:53 */
+  RAFT_FAULT_OVERFLOW = 4  /* log capacity exceeded (simulator limit) */
+};
+
+enum raft_variant { RAFT_VARIANT_VOTE_NO_LOG_CHECK = 1 /* drop core.clj:96,99 */ };
+
+/* Replaces `-main`'s argv (core.clj:197-200), the hard-coded timeouts (core.clj:173-174) and the
+ * chan buffer sizes (server.clj:37, client.clj:18). Defaults: raft_sim_default_config(). */
+typedef struct raft_sim_config {
+  uint32_t n_clusters;     /* clusters simulated by this handle */
+  uint32_t cluster_offset; /* global id of the first one (keys Philox: shard-invariant) */
+  uint32_t nodes;          /* N, 2..9 */
+  uint32_t log_cap;        /* L, max entries per log */
+  uint32_t arena_cap;      /* A >= 2L log-arena slots per node; 0 -> 4L */
+  uint32_t inbox_cap;      /* Q per queue, 1..16 */
+  uint64_t seed;
+  uint32_t hb, el_base, el_span;       /* 3000 / 5000 / 5000 ticks */
+  uint32_t drop_ppm, dup_ppm, dmin, dmax;
+  uint32_t part_ppm, part_epoch;
+  uint32_t client_ppm;
+  uint32_t variant_flags;
+  int32_t device;            /* HIP device ordinal */
+  uint32_t ticks_per_launch; /* ticks fused into one kernel launch; 0 -> default */
+  uint32_t reserved[4];
+} raft_sim_config_t;
+
+/* Canonical node record: the node map of init-node (core.clj:31-38) plus the log atom
+ * (log.clj:33-34) and simulator bookkeeping. next/match are indexed by id-1; 0 where absent. */
+typedef struct raft_node {
+  uint8_t role, voted_for, leader_id, fault;
+  uint8_t entries_is_seq, ls_present;
+  uint16_t votes;   /* bit i: id i in the :votes set */
+  uint16_t ls_keys; /* bit i: peer i has :next-index and :match-index keys */
+  uint16_t reserved0;
+  uint32_t current_term, commit_index, log_len, deadline;
+  int32_t next_index[RAFT_MAX_NODES];
+  int32_t match_index[RAFT_MAX_NODES];
+  uint32_t last_led_term;
+  uint32_t arena_base, arena_frontier;
+  uint32_t req_count, res_count; /* read-only: set through raft_sim_write_queue */
+  uint32_t reserved1;
+  uint64_t trace_hash;
+} raft_node_t;
+
+/* One queued message (SIM_SPEC §3): hdr = type | src<<3 | flag<<7 | epresent<<8 | pcnt<<16. */
+typedef struct raft_msg {
+  uint32_t arrival, hdr, term, a, b, eterm, eval, poff;
+} raft_msg_t;
+
+typedef struct raft_entry {
+  uint32_t term, val;
+} raft_entry_t;
+
+/* Cluster record of the leader-completeness checker (SIM_SPEC §4 P4). */
+typedef struct raft_hwm {
+  uint32_t index, term, val, reserved;
+} raft_hwm_t;
+
+enum raft_counter {
+  RAFT_CTR_EV_RV = 0, RAFT_CTR_EV_AE, RAFT_CTR_EV_CS, RAFT_CTR_EV_VR, RAFT_CTR_EV_AR,
+  RAFT_CTR_EV_TIMEOUT, RAFT_CTR_EV_HEARTBEAT, RAFT_CTR_LEADERS, RAFT_CTR_SENT,
+  RAFT_CTR_DELIVERED, RAFT_CTR_DROPPED, RAFT_CTR_PARTITIONED, RAFT_CTR_DUPLICATED,
+  RAFT_CTR_OVERFLOW, RAFT_CTR_TO_HALTED, RAFT_CTR_CLIENT_INJECTED, RAFT_CTR_HALT_IOOBE,
+  RAFT_CTR_HALT_NPE, RAFT_CTR_HALT_CCE, RAFT_CTR_HALT_OVERFLOW, RAFT_CTR_ENTRIES_APPENDED,
+  RAFT_CTR_ENTRIES_APPLIED, RAFT_CTR_PAYLOAD_EVICTED, RAFT_CTR_VIOL_ELECTION,
+  RAFT_CTR_VIOL_LOG, RAFT_CTR_VIOL_COMPLETE, RAFT_CTR_COUNT
+};
+
+typedef struct raft_counters {
+  uint64_t node_ticks;
+  uint64_t first_violation_tick; /* UINT64_MAX when none */
+  uint64_t c[RAFT_CTR_COUNT];
+} raft_counters_t;
+
+typedef struct raft_sim raft_sim_t;
+
+int raft_sim_abi_version(void);
+void raft_sim_default_config(raft_sim_config_t* cfg);
+
+/* Replaces raft-system + component/start (core.clj:23-29,201): allocates every cluster's nodes in
+ * HBM in the init-node state (core.clj:31-38) with empty logs (log.clj:33-34). */
+int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out);
+
+/* Replaces the `(loop [node ...] (recur (wait system node)))` of -main (core.clj:202-203) for every
+ * node of every cluster: advances all clusters by n_ticks (synchronous). */
+int raft_sim_step(raft_sim_t* sim, uint32_t n_ticks);
+
+/* Ticks simulated so far (the next tick to run). */
+uint64_t raft_sim_tick(const raft_sim_t* sim);
+
+/* Replaces `(prn node)` of wait (core.clj:182-183): canonical records, N per cluster. */
+int raft_sim_read_nodes(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_node_t* out);
+int raft_sim_write_nodes(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_node_t* in);
+
+/* The req-chan (which=0, server.clj:37) or resp-chan (which=1, client.clj:18) contents of node
+ * `node_id` (1..N), head first. read returns the count (>= 0) or a negative errno. */
+int raft_sim_read_queue(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, uint32_t which,
+                        raft_msg_t* out, uint32_t cap);
+int raft_sim_write_queue(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, uint32_t which,
+                         const raft_msg_t* in, uint32_t count);
+
+/* The raw log arena (arena_cap entries) behind the Log atom's :entries (log.clj:33-34). */
+int raft_sim_read_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, raft_entry_t* out,
+                        uint32_t cap);
+int raft_sim_write_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
+                         const raft_entry_t* in, uint32_t count);
+
+int raft_sim_read_hwm(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_hwm_t* out);
+int raft_sim_write_hwm(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_hwm_t* in);
+
+/* Counters of this handle's clusters (no reference counterpart; see SIM_SPEC §4). */
+int raft_sim_read_counters(raft_sim_t* sim, raft_counters_t* out);
+
+/* Per-cluster FNV-1a-64 digest of the canonical state (SIM_SPEC §6). */
+int raft_sim_digest(raft_sim_t* sim, uint32_t c0, uint32_t nc, uint64_t* out);
+
+/* Average device time of the last raft_sim_step's tick-kernel launches (HIP events on the
+ * simulator's stream) and their count; for bench.py's roofline. */
+int raft_sim_last_step_timing(raft_sim_t* sim, double* avg_kernel_ms, uint32_t* launches);
+
+void raft_sim_destroy(raft_sim_t* sim);
+const char* raft_sim_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFTSIM_H */

@@ -1,0 +1,638 @@
+"""Python restatement of angelini/raft-simulation's node state machine under SIM_SPEC.md.
+
+TEST INFRASTRUCTURE ONLY. Nothing in the product path (raft-simulation_amd/, include/) imports this
+module; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may. It is the
+independent, deliberately literal cross-check for the C oracle (oracle/raftref.c): Clojure maps
+become dicts, sets stay sets, `:keyword` states stay strings, exceptions become `Halt`. Each function
+cites the reference line it restates. AppendEntries payloads are real copies taken at send time (the
+ideal snapshot semantics); the C oracle and the kernel reference the sender's log arena instead and
+agree with this module whenever their `payload_evicted` counter is 0.
+
+Parity status: the reference ships no tests or golden vectors and needs a JVM that
+this image lacks, so this restatement is pinned by the hand-derived known-answer tests in
+tests/test_kat.py (each derived from the cited source lines) and by the Random123 Philox vectors.
+"""
+from __future__ import annotations
+
+M32 = 0xFFFFFFFF
+
+# ----------------------------------------------------------------------------------------------
+# Philox4x32-10 (Random123), SIM_SPEC §5
+# ----------------------------------------------------------------------------------------------
+PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
+PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+
+INIT, EVENT, NET, CLIENT, CLIENT_DETAIL, PART = 1, 2, 3, 4, 5, 6
+
+
+def philox(ctr, key):
+    c0, c1, c2, c3 = (x & M32 for x in ctr)
+    k0, k1 = key[0] & M32, key[1] & M32
+    for r in range(10):
+        p0 = PHILOX_M0 * c0
+        p1 = PHILOX_M1 * c2
+        hi0, lo0 = p0 >> 32, p0 & M32
+        hi1, lo1 = p1 >> 32, p1 & M32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0), lo1, (hi0 ^ c3 ^ k1), lo0
+        if r != 9:
+            k0 = (k0 + PHILOX_W0) & M32
+            k1 = (k1 + PHILOX_W1) & M32
+    return (c0, c1, c2, c3)
+
+
+def ppm(w):
+    return (w * 1000000) >> 32
+
+
+# ----------------------------------------------------------------------------------------------
+# FNV-1a-64 over u32 words (trace hash and digest, SIM_SPEC §4/§6)
+# ----------------------------------------------------------------------------------------------
+FNV_OFFSET = 0xCBF29CE484222325
+FNV_PRIME = 0x100000001B3
+M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def fnv(h, words):
+    for w in words:
+        h = ((h ^ (w & M32)) * FNV_PRIME) & M64
+    return h
+
+
+# ----------------------------------------------------------------------------------------------
+# Halts (SIM_SPEC §4, D8): the Clojure exception that kills the node's loop
+# ----------------------------------------------------------------------------------------------
+IOOBE, NPE, CCE, OVERFLOW = 1, 2, 3, 4
+
+
+class Halt(Exception):
+    def __init__(self, code):
+        super().__init__(code)
+        self.code = code
+
+
+# ----------------------------------------------------------------------------------------------
+# raft.log  (src/raft/log.clj)
+# ----------------------------------------------------------------------------------------------
+class Log:
+    """The log atom `{:entries [] :commit-index 0}` (log.clj:33-34) plus the LazySeq marker."""
+
+    def __init__(self, cap):
+        self.entries = []        # list of (term, val)
+        self.is_seq = False      # entries became a LazySeq through drop-last (log.clj:81)
+        self.commit_index = 0
+        self.cap = cap
+
+
+def val_at(entries, index):                       # log.clj:20-23
+    if index == 0:
+        return None
+    if index < 0 or index - 1 >= len(entries):    # (nth entries (- index 1)) out of range
+        raise Halt(IOOBE)
+    return entries[index - 1]
+
+
+def last_entry(log):                              # log.clj:47-49
+    return (log.commit_index, val_at(log.entries, log.commit_index))
+
+
+def entries_from(log, index):                     # log.clj:51-53
+    if log.is_seq:                                # subvec on a LazySeq
+        raise Halt(CCE)
+    return log.entries[min(index, len(log.entries)):]
+
+
+def compare_prev(log, prev_index, prev_term):     # log.clj:55-59
+    if prev_index == 0:
+        return True
+    return val_at(log.entries, prev_index) == prev_term
+
+
+def check_capacity(log, n):                       # SIM_SPEC §2 OVERFLOW (sim-only)
+    if len(log.entries) + n > log.cap:
+        raise Halt(OVERFLOW)
+
+
+def append_entries(log, entries):                 # log.clj:61-64
+    log.entries = log.entries + list(entries)     # (vec (concat ...))
+    log.is_seq = False
+
+
+def append_string_entries(log, term, vals):       # log.clj:66-67
+    append_entries(log, [(term, v) for v in vals])
+
+
+def apply_entries(log):                           # log.clj:69-76 + inc-commit-index 13-14
+    prev = log.commit_index
+    log.commit_index = len(log.entries)
+    return max(0, log.commit_index - prev)        # (take-last amount) -> written count
+
+
+def remove_from(log, index):                      # log.clj:78-81
+    keep = max(len(log.entries) - index, 0)
+    log.entries = log.entries[:keep]
+    log.is_seq = True
+
+
+# ----------------------------------------------------------------------------------------------
+# raft.core  (src/raft/core.clj)
+# ----------------------------------------------------------------------------------------------
+def majority(cluster, votes):                     # core.clj:19-21
+    cluster_size = len(cluster) + 1
+    return len(votes) >= -(-cluster_size // 2)    # (math/ceil (/ n 2))
+
+
+def init_node(id):                                # core.clj:31-38
+    return {"id": id, "state": ":follower", "current-term": 1, "voted-for": None,
+            "leader-id": None, "leader-state": None, "votes": set()}
+
+
+def leader_state(cluster, last_log_index):        # core.clj:40-42
+    return {"next-index": {p: last_log_index + 1 for p in cluster},
+            "match-index": {p: 0 for p in cluster}}
+
+
+def follower_to_candidate(node):                  # core.clj:69-73
+    n = dict(node)
+    n.update({"state": ":candidate", "voted-for": node["id"], "votes": {node["id"]},
+              "current-term": node["current-term"] + 1})
+    return n
+
+
+def candidate_to_follower(node):                  # core.clj:75-78  (sic :follwer)
+    n = dict(node)
+    n.update({"state": ":follwer", "voted-for": None, "votes": set()})
+    return n
+
+
+def candidate_to_leader(node):                    # core.clj:80-84
+    n = dict(node)
+    n.update({"state": ":leader", "voted-for": None, "votes": set(), "leader-id": node["id"]})
+    return n
+
+
+def leader_to_follower(node):                     # core.clj:86-89
+    n = dict(node)
+    n.update({"state": ":follower", "leader-id": None, "leader-state": None})
+    return n
+
+
+def request_vote_rpc(rpc, log, cluster, node):    # core.clj:48-54
+    last_index, last_term = last_entry(log)
+    msgs = [(p, {"type": "request-vote", "term": node["current-term"], "candidate-id": node["id"],
+                 "last-log-index": last_index, "last-log-term": last_term}) for p in cluster]
+    for p, m in msgs:
+        rpc(p, m)
+
+
+def append_entries_rpc(rpc, log, cluster, node):  # core.clj:56-67
+    last_index, _ = last_entry(log)
+    out = []
+    for p in cluster:
+        ls = node["leader-state"]
+        next_index = None if ls is None else ls["next-index"].get(p)
+        if next_index is None:                    # (- nil 1)
+            raise Halt(NPE)
+        prev_index = max(next_index - 1, 0)
+        entries = entries_from(log, prev_index)
+        out.append((p, {"type": "append-entries", "term": node["current-term"],
+                        "leader-id": node["id"], "leader-commit": last_index,
+                        "prev-log-index": prev_index,
+                        "prev-log-term": entries[0] if entries else None,
+                        "entries": list(entries[min(1, len(entries)):])}))
+    for p, m in out:
+        rpc(p, m)
+
+
+def request_vote_handler(log, message, node, respond, variant=0):   # core.clj:91-103
+    term, candidate_id = message["term"], message["candidate-id"]
+    response = {"term": node["current-term"], "id": node["id"], "type": "vote-response"}
+    consistent = True if variant & VOTE_NO_LOG_CHECK else \
+        compare_prev(log, message["last-log-index"], message["last-log-term"])
+    if term < node["current-term"] or node["voted-for"] is not None or not consistent:
+        respond(dict(response, **{"vote-granted": False}))
+        return node
+    respond(dict(response, **{"vote-granted": True}))
+    n = dict(node)
+    n["voted-for"] = candidate_id
+    return n
+
+
+def append_entries_handler(log, message, node, respond, stats):     # core.clj:105-123
+    term, prev_index = message["term"], message["prev-log-index"]
+    response = {"term": node["current-term"], "id": node["id"], "type": "append-response"}
+    consistent = compare_prev(log, prev_index, message["prev-log-term"])
+    if term < node["current-term"]:
+        respond(dict(response, success=False))
+        return node
+    if not consistent:
+        respond(dict(response, success=False))
+        remove_from(log, prev_index)
+        return node
+    check_capacity(log, len(message["entries"]))
+    stats["appended_at"] = len(log.entries)
+    append_entries(log, message["entries"])
+    stats["entries_appended"] += len(message["entries"])
+    stats["entries_applied"] += apply_entries(log)
+    respond(dict(response, success=True, commit=message["leader-commit"],
+                 **{"log-index": prev_index + len(message["entries"])}))
+    n = candidate_to_follower(node)
+    n["leader-id"] = message["leader-id"]
+    n["current-term"] = term
+    return n
+
+
+def vote_response_handler(rpc, log, cluster, message, node, stats):  # core.clj:125-139
+    term, granted, id = message["term"], message["vote-granted"], message["id"]
+    last_log_index = last_entry(log)[0]
+    if term > node["current-term"]:
+        n = dict(node)
+        n["current-term"] = term
+        return candidate_to_follower(n)
+    if not granted:
+        return node
+    if node["state"] != ":candidate":
+        return node
+    votes = node["votes"] | {id}
+    if not majority(cluster, votes):
+        n = dict(node)
+        n["votes"] = votes
+        return n
+    n = candidate_to_leader(node)
+    n["leader-state"] = leader_state(cluster, last_log_index)
+    append_entries_rpc(rpc, log, cluster, n)
+    stats["elected"] = True
+    return n
+
+
+def append_response_handler(message, node, stats):                   # core.clj:141-149
+    term, success, id = message["term"], message["success"], message["id"]
+    if term > node["current-term"]:
+        n = dict(node)
+        n["current-term"] = term
+        return leader_to_follower(n)
+    if not success:
+        ls = node["leader-state"]
+        if ls is None or ls["next-index"].get(id) is None:           # (dec nil)
+            raise Halt(NPE)
+        n = dict(node)
+        n["leader-state"] = {"next-index": dict(ls["next-index"]),
+                             "match-index": dict(ls["match-index"])}
+        n["leader-state"]["next-index"][id] -= 1
+        return n
+    ls = node["leader-state"] or {}
+    n = dict(node)
+    n["leader-state"] = {"next-index": dict(ls.get("next-index", {})),
+                         "match-index": dict(ls.get("match-index", {}))}
+    n["leader-state"]["next-index"][id] = message["log-index"]
+    n["leader-state"]["match-index"][id] = message["commit"]
+    stats["match_changed"] = True
+    return n
+
+
+def client_set_handler(log, message, node, stats):                   # core.clj:151-160
+    if node["state"] != ":leader":
+        return node                                # redirect-client: no state change
+    check_capacity(log, 1)
+    stats["appended_at"] = len(log.entries)
+    append_string_entries(log, node["current-term"], [message["command"]])
+    stats["entries_appended"] += 1
+    return node
+
+
+def heartbeat_handler(rpc, log, cluster, node):                      # core.clj:162-164
+    append_entries_rpc(rpc, log, cluster, node)
+    return node
+
+
+def timeout_handler(rpc, log, cluster, node):                        # core.clj:166-169
+    new_node = follower_to_candidate(node)
+    request_vote_rpc(rpc, log, cluster, new_node)
+    return new_node
+
+
+# ----------------------------------------------------------------------------------------------
+# Tick engine (SIM_SPEC §4): the lockstep restatement of wait (core.clj:176-195)
+# ----------------------------------------------------------------------------------------------
+VOTE_NO_LOG_CHECK = 1
+
+TYPE_CODE = {"request-vote": 1, "append-entries": 2, "client-set": 3,
+             "vote-response": 4, "append-response": 5}
+REQ_TYPES = (1, 2, 3)
+ROLE_CODE = {":follower": 0, ":candidate": 1, ":leader": 2, ":follwer": 3}
+
+COUNTERS = ["ev_rv", "ev_ae", "ev_cs", "ev_vr", "ev_ar", "ev_timeout", "ev_heartbeat",
+            "leaders", "sent", "delivered", "dropped", "partitioned", "duplicated", "overflow",
+            "to_halted", "client_injected", "halt_ioobe", "halt_npe", "halt_cce",
+            "halt_overflow", "entries_appended", "entries_applied", "payload_evicted",
+            "viol_election", "viol_log", "viol_complete"]
+
+
+def default_config(**kw):
+    cfg = dict(nodes=5, log_cap=64, arena_cap=0, inbox_cap=16, seed=42, hb=3000, el_base=5000,
+               el_span=5000, drop_ppm=0, dup_ppm=0, dmin=1, dmax=1, part_ppm=0, part_epoch=1000,
+               client_ppm=0, variant_flags=0)
+    cfg.update(kw)
+    return cfg
+
+
+def msg_src(m):
+    t = m["type"]
+    if t == "request-vote":
+        return m["candidate-id"]
+    if t == "append-entries":
+        return m["leader-id"]
+    if t == "client-set":
+        return 0
+    return m["id"]
+
+
+class PyCluster:
+    """One cluster of N nodes; `step(t)` runs phases P0-P4 of SIM_SPEC §4 for tick t."""
+
+    def __init__(self, cfg, gid):
+        self.cfg = cfg
+        self.N = cfg["nodes"]
+        self.gid = gid
+        self.key = (cfg["seed"] & M32, (cfg["seed"] >> 32) & M32)
+        ids = list(range(1, self.N + 1))
+        self.cluster = {i: [p for p in ids if p != i] for i in ids}
+        self.nodes = {i: init_node(i) for i in ids}
+        self.logs = {i: Log(cfg["log_cap"]) for i in ids}
+        self.req = {i: [] for i in ids}   # list of (arrival, msg)
+        self.res = {i: [] for i in ids}
+        self.fault = {i: 0 for i in ids}
+        self.trace = {i: FNV_OFFSET for i in ids}
+        self.last_led = {i: 0 for i in ids}
+        self.hwm = (0, 0, 0)
+        self.cnt = {k: 0 for k in COUNTERS}
+        self.first_violation = None
+        self.deadline = {}
+        for i in ids:
+            w = philox((gid, i | INIT << 8, 0, 0), self.key)
+            self.deadline[i] = cfg["el_base"] + ((w[1] * cfg["el_span"]) >> 32)
+
+    # -- network ---------------------------------------------------------------------------
+    def insert(self, r, arrival, msg):
+        q = self.req[r] if TYPE_CODE[msg["type"]] in REQ_TYPES else self.res[r]
+        if self.fault[r]:
+            self.cnt["to_halted"] += 1
+            return
+        if len(q) >= self.cfg["inbox_cap"]:
+            self.cnt["overflow"] += 1
+            return
+        pos = len(q)
+        while pos > 0 and q[pos - 1][0] > arrival:
+            pos -= 1
+        q.insert(pos, (arrival, msg))
+        self.cnt["delivered"] += 1
+
+    def partition_sides(self, t):
+        cfg = self.cfg
+        if cfg["part_ppm"] == 0:
+            return None
+        p = philox((self.gid, PART << 8, t // cfg["part_epoch"], 0), self.key)
+        if ppm(p[0]) >= cfg["part_ppm"]:
+            return None
+        return p[1]
+
+    def transmit(self, s, r, t, msg, outbox, sides):
+        """P2 fault draws for one emitted message (SIM_SPEC §4 P2)."""
+        cfg = self.cfg
+        self.cnt["sent"] += 1
+        if sides is not None and ((sides >> s) & 1) != ((sides >> r) & 1):
+            self.cnt["partitioned"] += 1
+            return
+        faulty = cfg["drop_ppm"] or cfg["dup_ppm"] or cfg["dmin"] != cfg["dmax"]
+        if not faulty:
+            outbox.setdefault(r, []).append((s, [(t + cfg["dmin"], msg)]))
+            return
+        w = philox((self.gid, s | NET << 8, t, r), self.key)
+        if ppm(w[0]) < cfg["drop_ppm"]:
+            self.cnt["dropped"] += 1
+            return
+        span = cfg["dmax"] - cfg["dmin"] + 1
+        copies = [(t + cfg["dmin"] + ((w[2] * span) >> 32), msg)]
+        if ppm(w[1]) < cfg["dup_ppm"]:
+            self.cnt["duplicated"] += 1
+            copies.append((t + cfg["dmin"] + ((w[3] * span) >> 32), msg))
+        outbox.setdefault(r, []).append((s, copies))
+
+    # -- one tick --------------------------------------------------------------------------
+    def step(self, t):
+        cfg, N = self.cfg, self.N
+        # P0 client injection
+        if cfg["client_ppm"]:
+            w = philox((self.gid, CLIENT << 8, t >> 2, 0), self.key)
+            if ppm(w[t & 3]) < cfg["client_ppm"]:
+                d = philox((self.gid, CLIENT_DETAIL << 8, t, 0), self.key)
+                target = 1 + ((d[0] * N) >> 32)
+                self.cnt["client_injected"] += 1
+                self.insert(target, t, {"type": "client-set", "command": d[1]})
+        sides = self.partition_sides(t)
+        outbox = {}
+        elected, appended, match_changed = {}, {}, set()
+        hwm_before = self.hwm
+        # P1 events
+        for i in range(1, N + 1):
+            if self.fault[i]:
+                continue
+            req_ok = bool(self.req[i]) and self.req[i][0][0] <= t
+            res_ok = bool(self.res[i]) and self.res[i][0][0] <= t
+            if not (req_ok or res_ok or t >= self.deadline[i]):
+                continue
+            w = philox((self.gid, i | EVENT << 8, t, 0), self.key)
+            if req_ok and res_ok:
+                q = self.res[i] if (w[0] & 1) else self.req[i]
+            elif req_ok:
+                q = self.req[i]
+            elif res_ok:
+                q = self.res[i]
+            else:
+                q = None
+            node, log = self.nodes[i], self.logs[i]
+            msg = q.pop(0)[1] if q is not None else None
+            sends = []
+
+            def rpc(p, m, sends=sends):
+                sends.append((p, m))
+
+            def respond(body, sends=sends, msg=msg):
+                sends.append((msg_src(msg), body))
+
+            stats = {"entries_appended": 0, "entries_applied": 0, "appended_at": None,
+                     "elected": False, "match_changed": False}
+            cluster = self.cluster[i]
+            try:
+                if msg is None:
+                    if node["state"] == ":leader":
+                        ev = 7
+                        new = heartbeat_handler(rpc, log, cluster, node)
+                    else:
+                        ev = 6
+                        new = timeout_handler(rpc, log, cluster, node)
+                else:
+                    ev = TYPE_CODE[msg["type"]]
+                    if ev == 1:
+                        new = request_vote_handler(log, msg, node, respond, cfg["variant_flags"])
+                    elif ev == 2:
+                        new = append_entries_handler(log, msg, node, respond, stats)
+                    elif ev == 3:
+                        new = client_set_handler(log, msg, node, stats)
+                    elif ev == 4:
+                        new = vote_response_handler(rpc, log, cluster, msg, node, stats)
+                    else:
+                        new = append_response_handler(msg, node, stats)
+            except Halt as h:
+                self.fault[i] = h.code
+                self.cnt[["", "halt_ioobe", "halt_npe", "halt_cce", "halt_overflow"][h.code]] += 1
+                self.trace[i] = fnv(self.trace[i], self._trace_words(t, ev, msg, node, h.code))
+                continue
+            self.nodes[i] = new
+            self.cnt[COUNTERS[ev - 1]] += 1
+            self.cnt["entries_appended"] += stats["entries_appended"]
+            self.cnt["entries_applied"] += stats["entries_applied"]
+            if stats["appended_at"] is not None and len(log.entries) > stats["appended_at"]:
+                appended[i] = stats["appended_at"]
+            if stats["elected"]:
+                self.cnt["leaders"] += 1
+                self.last_led[i] = new["current-term"]
+                elected[i] = new["current-term"]
+            if stats["match_changed"]:
+                match_changed.add(i)
+            if new["state"] == ":leader":
+                self.deadline[i] = t + cfg["hb"]
+            else:
+                self.deadline[i] = t + cfg["el_base"] + ((w[1] * cfg["el_span"]) >> 32)
+            self.trace[i] = fnv(self.trace[i], self._trace_words(t, ev, msg, new, 0))
+            for p, m in sends:
+                self.transmit(i, p, t, m, outbox, sides)
+        # P2 delivery: receiver order, then sender id ascending, copy 0 then copy 1
+        for r in sorted(outbox):
+            for s, copies in sorted(outbox[r], key=lambda x: x[0]):
+                for arrival, m in copies:
+                    self.insert(r, arrival, m)
+        # P3 is implicit here: payloads were snapshotted at send time and appended in P1.
+        # P4 invariant checker
+        self._check(t, elected, appended, match_changed, hwm_before)
+
+    def _trace_words(self, t, ev, msg, node, fault):
+        src = msg_src(msg) if msg is not None else 0
+        mterm = msg.get("term", 0) if msg is not None else 0
+        return [t, ev, src, mterm, ROLE_CODE[node["state"]], node["current-term"], fault]
+
+    def _violation(self, kind, t):
+        self.cnt[kind] += 1
+        if self.first_violation is None or t < self.first_violation:
+            self.first_violation = t
+
+    def _check(self, t, elected, appended, match_changed, hwm_before):
+        N = self.N
+        for i in sorted(elected):
+            T = elected[i]
+            if any(self.last_led[j] == T for j in range(1, N + 1) if j != i):
+                self._violation("viol_election", t)
+        for i in sorted(appended):
+            a, li = appended[i], self.logs[i].entries
+            bad = False
+            for j in range(1, N + 1):
+                if j == i or bad:
+                    continue
+                lj = self.logs[j].entries
+                for k in range(a, min(len(li), len(lj))):
+                    if li[k][0] == lj[k][0] and li[k][1] != lj[k][1]:
+                        bad = True
+                        break
+            if bad:
+                self._violation("viol_log", t)
+        hidx, hterm, hval = hwm_before
+        for i in sorted(elected):
+            if hidx > 0:
+                li = self.logs[i].entries
+                if len(li) < hidx or li[hidx - 1] != (hterm, hval):
+                    self._violation("viol_complete", t)
+        best = None
+        for i in range(1, N + 1):
+            node = self.nodes[i]
+            if node["state"] != ":leader" or (i not in elected and i not in match_changed):
+                continue
+            ls = node["leader-state"] or {"match-index": {}}
+            li = self.logs[i].entries
+            vals = [len(li)] + [s32(ls["match-index"].get(p, 0)) for p in self.cluster[i]]
+            vals.sort(reverse=True)
+            m = min(vals[(N + 1) // 2 - 1], len(li))
+            if m > self.hwm[0] and (best is None or m > best[0]):
+                best = (m, li[m - 1][0], li[m - 1][1])
+        if best is not None:
+            self.hwm = best
+
+    # -- canonical export (matches raft_node_t / raft_msg_t of include/raftsim.h) -----------
+    def canonical_node(self, i):
+        node, log = self.nodes[i], self.logs[i]
+        ls = node["leader-state"]
+        keys = 0
+        nxt, mch = [0] * self.N, [0] * self.N
+        if ls is not None:
+            for p in set(ls["next-index"]) | set(ls["match-index"]):
+                keys |= 1 << p
+                nxt[p - 1] = s32(ls["next-index"].get(p, 0))
+                mch[p - 1] = s32(ls["match-index"].get(p, 0))
+        votes = 0
+        for v in node["votes"]:
+            votes |= 1 << v
+        return {"role": ROLE_CODE[node["state"]], "voted_for": node["voted-for"] or 0,
+                "leader_id": node["leader-id"] or 0, "fault": self.fault[i],
+                "entries_is_seq": int(log.is_seq), "ls_present": int(ls is not None),
+                "votes": votes, "ls_keys": keys, "current_term": node["current-term"] & M32,
+                "commit_index": log.commit_index & M32, "log_len": len(log.entries),
+                "deadline": self.deadline[i] & M32, "next_index": nxt, "match_index": mch,
+                "last_led_term": self.last_led[i], "trace_hash": self.trace[i],
+                "req_count": len(self.req[i]), "res_count": len(self.res[i])}
+
+    def canonical_msgs(self, i, which):
+        q = self.req[i] if which == 0 else self.res[i]
+        return [encode_msg(arr, m) for arr, m in q]
+
+
+def s32(x):
+    x &= M32
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def encode_msg(arrival, m):
+    """Message -> (arrival, hdr, term, a, b, eterm, eval, pcnt, payload) (SIM_SPEC §3).
+
+    The payload is returned as a list so callers can compare it with the arena contents the C/HIP
+    implementations reference through `poff`."""
+    code = TYPE_CODE[m["type"]]
+    src = msg_src(m)
+    flag = epresent = 0
+    term = a = b = eterm = evalue = 0
+    payload = []
+    if code == 1:
+        term, a = m["term"], m["last-log-index"]
+        e = m["last-log-term"]
+    elif code == 2:
+        term, a, b = m["term"], m["leader-commit"], m["prev-log-index"]
+        e = m["prev-log-term"]
+        payload = list(m["entries"])
+    else:
+        e = None
+        if code == 3:
+            a = m["command"]
+        elif code == 4:
+            term, flag = m["term"], int(m["vote-granted"])
+        else:
+            term, flag = m["term"], int(m["success"])
+            if m["success"]:
+                a, b = m["commit"], m["log-index"]
+    if e is not None:
+        epresent, eterm, evalue = 1, e[0], e[1]
+    hdr = code | src << 3 | flag << 7 | epresent << 8 | len(payload) << 16
+    return (arrival & M32, hdr, term & M32, a & M32, b & M32, eterm & M32, evalue & M32, payload)
+
+
+def run(cfg, gid, ticks, t0=0):
+    c = PyCluster(cfg, gid)
+    for t in range(t0, t0 + ticks):
+        c.step(t)
+    return c

@@ -1,0 +1,830 @@
+/* raftref.c — CPU oracle (and CPU baseline) for the batched Raft simulator.
+ * TEST INFRASTRUCTURE ONLY: see raftref.h. Semantics: SIM_SPEC.md; every handler cites the
+ * reference line it restates. Clusters are independent, so raft_ref_step maps over contiguous
+ * cluster chunks with one pthread each (the `pmap` analogue of SURVEY.md §8d) and runs each
+ * cluster's ticks back to back.
+ */
+#include "raftref.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static __thread char g_err[256];
+static int fail(int code, const char* msg) {
+  snprintf(g_err, sizeof g_err, "%s", msg);
+  return code;
+}
+const char* raft_ref_last_error(void) { return g_err; }
+
+/* ---------------------------------------------------------------- Philox4x32-10 (SIM_SPEC §5) */
+enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_CLIENT_DETAIL = 5, P_PART = 6 };
+
+void raft_ref_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
+                 uint32_t w[4]);
+static uint32_t ppm(uint32_t w) { return (uint32_t)(((uint64_t)w * 1000000u) >> 32); }
+
+/* ---------------------------------------------------------------- FNV-1a-64 over u32 words */
+#define FNV_OFFSET 0xCBF29CE484222325ull
+#define FNV_PRIME 0x100000001B3ull
+static uint64_t fnv(uint64_t h, uint32_t w) { return (h ^ w) * FNV_PRIME; }
+
+/* ---------------------------------------------------------------- simulator state */
+struct raft_ref {
+  raft_sim_config_t cfg;
+  uint32_t N, Q, L, A, C;
+  uint32_t key[2];
+  uint64_t tick;
+  raft_node_t* nodes;   /* [C*N] */
+  raft_msg_t* q;        /* [C*N][2][Q], index 0 = head */
+  raft_entry_t* arena;  /* [C*N][A] */
+  raft_hwm_t* hwm;      /* [C] */
+  raft_counters_t ctr;
+  int threads;
+};
+
+static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
+                 uint32_t w[4]) {
+  uint32_t ctr[4] = {g, nodep, t, x};
+  raft_ref_philox(ctr, s->key, w);
+}
+
+void raft_ref_default_config(raft_sim_config_t* c) {
+  memset(c, 0, sizeof *c);
+  c->n_clusters = 1; c->nodes = 5; c->log_cap = 64; c->inbox_cap = 16; c->seed = 42;
+  c->hb = 3000; c->el_base = 5000; c->el_span = 5000; c->dmin = 1; c->dmax = 1;
+  c->part_epoch = 1000;
+}
+
+static raft_msg_t* qslot(raft_ref_t* s, uint32_t gi, int which) {
+  return s->q + ((size_t)gi * 2 + which) * s->Q;
+}
+static raft_entry_t* arena_of(raft_ref_t* s, uint32_t gi) { return s->arena + (size_t)gi * s->A; }
+
+static int validate_cfg(const raft_sim_config_t* c) {
+  if (c->nodes < 2 || c->nodes > RAFT_MAX_NODES) return fail(-EINVAL, "nodes must be 2..9");
+  if (c->n_clusters == 0) return fail(-EINVAL, "n_clusters must be > 0");
+  if (c->inbox_cap < 1 || c->inbox_cap > RAFT_MAX_INBOX) return fail(-EINVAL, "inbox_cap 1..16");
+  if (c->log_cap < 1 || c->log_cap > 65535) return fail(-EINVAL, "log_cap 1..65535");
+  uint64_t A = c->arena_cap ? c->arena_cap : 4ull * c->log_cap;
+  if (A < 2ull * c->log_cap || A > (1u << 24)) return fail(-EINVAL, "arena_cap must be >= 2*log_cap");
+  if (c->hb < 1 || c->el_base < 1) return fail(-EINVAL, "hb and el_base must be >= 1");
+  if (c->dmin < 1 || c->dmax < c->dmin || c->dmax > 255) return fail(-EINVAL, "1 <= dmin <= dmax <= 255");
+  if (c->part_epoch < 1) return fail(-EINVAL, "part_epoch must be >= 1");
+  if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
+      c->client_ppm > 1000000) return fail(-EINVAL, "ppm values must be <= 1e6");
+  return 0;
+}
+
+int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
+  if (!cfg || !out) return fail(-EINVAL, "null argument");
+  int rc = validate_cfg(cfg);
+  if (rc) return rc;
+  raft_ref_t* s = (raft_ref_t*)calloc(1, sizeof *s);
+  if (!s) return fail(-ENOMEM, "oom");
+  s->cfg = *cfg;
+  s->N = cfg->nodes; s->Q = cfg->inbox_cap; s->L = cfg->log_cap; s->C = cfg->n_clusters;
+  s->A = cfg->arena_cap ? cfg->arena_cap : 4 * cfg->log_cap;
+  s->key[0] = (uint32_t)cfg->seed; s->key[1] = (uint32_t)(cfg->seed >> 32);
+  s->threads = 1;
+  size_t nn = (size_t)s->C * s->N;
+  s->nodes = (raft_node_t*)calloc(nn, sizeof(raft_node_t));
+  s->q = (raft_msg_t*)calloc(nn * 2 * s->Q, sizeof(raft_msg_t));
+  s->arena = (raft_entry_t*)calloc(nn * s->A, sizeof(raft_entry_t));
+  s->hwm = (raft_hwm_t*)calloc(s->C, sizeof(raft_hwm_t));
+  if (!s->nodes || !s->q || !s->arena || !s->hwm) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+  for (uint32_t c = 0; c < s->C; ++c) {
+    uint32_t g = cfg->cluster_offset + c;
+    for (uint32_t k = 0; k < s->N; ++k) {
+      raft_node_t* n = &s->nodes[(size_t)c * s->N + k];
+      n->role = RAFT_FOLLOWER;      /* init-node, core.clj:31-38 */
+      n->current_term = 1;
+      n->trace_hash = FNV_OFFSET;
+      uint32_t w[4];
+      draw(s, g, (k + 1) | P_INIT << 8, 0, 0, w);
+      n->deadline = cfg->el_base + (uint32_t)(((uint64_t)w[1] * cfg->el_span) >> 32);
+    }
+  }
+  s->ctr.first_violation_tick = UINT64_MAX;
+  *out = s;
+  return 0;
+}
+
+int raft_ref_set_threads(raft_ref_t* s, int threads) {
+  if (!s || threads < 1 || threads > 1024) return fail(-EINVAL, "threads 1..1024");
+  s->threads = threads;
+  return 0;
+}
+
+void raft_ref_destroy(raft_ref_t* s) {
+  if (!s) return;
+  free(s->nodes); free(s->q); free(s->arena); free(s->hwm); free(s);
+}
+
+uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
+
+/* ---------------------------------------------------------------- per-cluster tick */
+typedef struct {
+  uint64_t c[RAFT_CTR_COUNT];
+  uint64_t first_violation;
+} local_ctr_t;
+
+typedef struct { int n; uint32_t arr[2]; raft_msg_t m; } cell_t;
+
+enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
+typedef struct {
+  int kind, reloc;
+  uint32_t old_base, old_len, src, poff, pcnt;
+  raft_entry_t entry;
+} plan_t;
+
+typedef struct {
+  raft_ref_t* s;
+  uint32_t c, g, t, N;
+  raft_node_t* nodes;
+  local_ctr_t* lc;
+  cell_t cell[RAFT_MAX_NODES][RAFT_MAX_NODES]; /* [src-1][dst-1] */
+  int part;
+  uint32_t sides;
+} tick_ctx_t;
+
+static void violation(tick_ctx_t* x, int kind) {
+  x->lc->c[kind]++;
+  if (x->t < x->lc->first_violation) x->lc->first_violation = x->t;
+}
+
+/* val-at (log.clj:20-23) on node k's log; returns a fault code or 0. */
+static int val_at(tick_ctx_t* x, uint32_t k, uint32_t idx, int* present, raft_entry_t* e) {
+  raft_node_t* n = &x->nodes[k];
+  if (idx == 0) { *present = 0; return 0; }
+  if (idx > n->log_len) return RAFT_FAULT_IOOBE;
+  *e = arena_of(x->s, x->c * x->N + k)[(n->arena_base + idx - 1) % x->s->A];
+  *present = 1;
+  return 0;
+}
+
+/* compare-prev? (log.clj:55-59): whole-entry equality, nil never equal. */
+static int compare_prev(tick_ctx_t* x, uint32_t k, uint32_t idx, const raft_msg_t* m, int* out) {
+  if (idx == 0) { *out = 1; return 0; }
+  int present; raft_entry_t e;
+  int f = val_at(x, k, idx, &present, &e);
+  if (f) return f;
+  int mpresent = (m->hdr >> 8) & 1;
+  *out = mpresent && present && e.term == m->eterm && e.val == m->eval;
+  return 0;
+}
+
+static uint32_t hdr(uint32_t type, uint32_t src, uint32_t flag, uint32_t epresent, uint32_t pcnt) {
+  return type | src << 3 | flag << 7 | epresent << 8 | pcnt << 16;
+}
+
+typedef struct { uint32_t dst; raft_msg_t m; } emit_t;
+
+/* append-entries-rpc (core.clj:56-67) from the (post-transition) record nn of node k. */
+static int ae_broadcast(tick_ctx_t* x, uint32_t k, const raft_node_t* nn, emit_t* em, int* ne) {
+  uint32_t id = k + 1;
+  int present; raft_entry_t e;
+  int f = val_at(x, k, nn->commit_index, &present, &e);   /* last-entry, log.clj:47-49 */
+  if (f) return f;
+  for (uint32_t p = 1; p <= x->N; ++p) {
+    if (p == id) continue;
+    if (!nn->ls_present || !((nn->ls_keys >> p) & 1)) return RAFT_FAULT_NPE; /* (- nil 1) */
+    if (nn->entries_is_seq) return RAFT_FAULT_CCE;                         /* subvec LazySeq */
+  }
+  const raft_entry_t* ar = arena_of(x->s, x->c * x->N + k);
+  for (uint32_t p = 1; p <= x->N; ++p) {
+    if (p == id) continue;
+    int32_t next = nn->next_index[p - 1];
+    int32_t prev = next - 1 > 0 ? next - 1 : 0;
+    uint32_t start = (uint32_t)prev < nn->log_len ? (uint32_t)prev : nn->log_len;
+    raft_msg_t m = {0};
+    m.term = nn->current_term;
+    m.a = nn->commit_index;
+    m.b = (uint32_t)prev;
+    uint32_t pcnt = 0, ep = 0;
+    if (start < nn->log_len) {
+      raft_entry_t pe = ar[(nn->arena_base + start) % x->s->A];
+      ep = 1; m.eterm = pe.term; m.eval = pe.val;
+      pcnt = nn->log_len - start - 1;
+    }
+    m.poff = pcnt ? nn->arena_base + start + 1 : 0;
+    m.hdr = hdr(RAFT_MSG_APPEND_ENTRIES, id, 0, ep, pcnt);
+    em[*ne].dst = p; em[*ne].m = m; (*ne)++;
+  }
+  return 0;
+}
+
+/* Plan an append of m entries to node record nn (SIM_SPEC §4 P3: relocation on a dead tail). */
+static void plan_append(tick_ctx_t* x, raft_node_t* nn, plan_t* pl, uint32_t m) {
+  (void)x;
+  pl->old_base = nn->arena_base;
+  pl->old_len = nn->log_len;
+  pl->reloc = 0;
+  if (m > 0) {
+    if (nn->arena_base + nn->log_len != nn->arena_frontier) {
+      pl->reloc = 1;
+      nn->arena_base = nn->arena_frontier;
+      nn->arena_frontier += nn->log_len;
+    }
+    nn->arena_frontier += m;
+  }
+  nn->log_len += m;
+  nn->entries_is_seq = 0; /* (vec (concat ...)), log.clj:64 */
+}
+
+static void queue_insert(tick_ctx_t* x, uint32_t k, const raft_msg_t* m) {
+  raft_ref_t* s = x->s;
+  raft_node_t* n = &x->nodes[k];
+  uint32_t type = m->hdr & 7;
+  int which = type <= RAFT_MSG_CLIENT_SET ? 0 : 1;
+  if (n->fault) { x->lc->c[RAFT_CTR_TO_HALTED]++; return; }
+  uint32_t* cnt = which ? &n->res_count : &n->req_count;
+  if (*cnt >= s->Q) { x->lc->c[RAFT_CTR_OVERFLOW]++; return; }
+  raft_msg_t* q = qslot(s, x->c * x->N + k, which);
+  uint32_t pos = *cnt;
+  while (pos > 0 && q[pos - 1].arrival > m->arrival) { q[pos] = q[pos - 1]; --pos; }
+  q[pos] = *m;
+  (*cnt)++;
+  x->lc->c[RAFT_CTR_DELIVERED]++;
+}
+
+/* Network (SIM_SPEC §4 P2): faults for one emitted message s->r. */
+static void transmit(tick_ctx_t* x, uint32_t s_id, uint32_t r_id, const raft_msg_t* m) {
+  const raft_sim_config_t* cfg = &x->s->cfg;
+  x->lc->c[RAFT_CTR_SENT]++;
+  if (x->part && (((x->sides >> s_id) ^ (x->sides >> r_id)) & 1)) {
+    x->lc->c[RAFT_CTR_PARTITIONED]++;
+    return;
+  }
+  cell_t* cl = &x->cell[s_id - 1][r_id - 1];
+  cl->m = *m;
+  if (!cfg->drop_ppm && !cfg->dup_ppm && cfg->dmin == cfg->dmax) {
+    cl->n = 1; cl->arr[0] = x->t + cfg->dmin;
+    return;
+  }
+  uint32_t w[4];
+  draw(x->s, x->g, s_id | P_NET << 8, x->t, r_id, w);
+  if (ppm(w[0]) < cfg->drop_ppm) { x->lc->c[RAFT_CTR_DROPPED]++; return; }
+  uint32_t span = cfg->dmax - cfg->dmin + 1;
+  cl->n = 1;
+  cl->arr[0] = x->t + cfg->dmin + (uint32_t)(((uint64_t)w[2] * span) >> 32);
+  if (ppm(w[1]) < cfg->dup_ppm) {
+    x->lc->c[RAFT_CTR_DUPLICATED]++;
+    cl->n = 2;
+    cl->arr[1] = x->t + cfg->dmin + (uint32_t)(((uint64_t)w[3] * span) >> 32);
+  }
+}
+
+static uint64_t trace(uint64_t h, uint32_t t, uint32_t ev, uint32_t src, uint32_t mterm,
+                      const raft_node_t* n, uint32_t fault) {
+  h = fnv(h, t); h = fnv(h, ev); h = fnv(h, src); h = fnv(h, mterm);
+  h = fnv(h, n->role); h = fnv(h, n->current_term); h = fnv(h, fault);
+  return h;
+}
+
+static uint32_t popcount16(uint32_t v) { return (uint32_t)__builtin_popcount(v & 0xFFFF); }
+
+static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc) {
+  const raft_sim_config_t* cfg = &s->cfg;
+  tick_ctx_t X;
+  tick_ctx_t* x = &X;
+  x->s = s; x->c = c; x->g = cfg->cluster_offset + c; x->t = t; x->N = s->N;
+  x->nodes = s->nodes + (size_t)c * s->N; x->lc = lc;
+  memset(x->cell, 0, sizeof x->cell);
+  const uint32_t N = s->N;
+  uint32_t w[4];
+
+  /* P0 client injection (D9) */
+  if (cfg->client_ppm) {
+    draw(s, x->g, P_CLIENT << 8, t >> 2, 0, w);
+    if (ppm(w[t & 3]) < cfg->client_ppm) {
+      uint32_t d[4];
+      draw(s, x->g, P_CLIENT_DETAIL << 8, t, 0, d);
+      uint32_t target = 1 + (uint32_t)(((uint64_t)d[0] * N) >> 32);
+      raft_msg_t m = {0};
+      m.arrival = t; m.hdr = hdr(RAFT_MSG_CLIENT_SET, 0, 0, 0, 0); m.a = d[1];
+      lc->c[RAFT_CTR_CLIENT_INJECTED]++;
+      queue_insert(x, target - 1, &m);
+    }
+  }
+  x->part = 0; x->sides = 0;
+  if (cfg->part_ppm) {
+    draw(s, x->g, P_PART << 8, t / cfg->part_epoch, 0, w);
+    if (ppm(w[0]) < cfg->part_ppm) { x->part = 1; x->sides = w[1]; }
+  }
+
+  plan_t plan[RAFT_MAX_NODES];
+  int appended_at[RAFT_MAX_NODES];
+  uint32_t elected = 0, match_changed = 0;
+  raft_hwm_t hwm0 = s->hwm[c];
+  memset(plan, 0, sizeof plan);
+  for (uint32_t k = 0; k < N; ++k) appended_at[k] = -1;
+
+  /* P1 one event per running node (wait, core.clj:176-195) */
+  for (uint32_t k = 0; k < N; ++k) {
+    raft_node_t* n = &x->nodes[k];
+    if (n->fault) continue;
+    uint32_t gi = c * N + k, id = k + 1;
+    raft_msg_t* rq = qslot(s, gi, 0);
+    raft_msg_t* rs = qslot(s, gi, 1);
+    int req_ok = n->req_count && rq[0].arrival <= t;
+    int res_ok = n->res_count && rs[0].arrival <= t;
+    if (!req_ok && !res_ok && t < n->deadline) continue;
+    draw(s, x->g, id | P_EVENT << 8, t, 0, w);
+    int which = -1;
+    if (req_ok && res_ok) which = (w[0] & 1) ? 1 : 0;   /* alts!! choice, core.clj:181 */
+    else if (req_ok) which = 0;
+    else if (res_ok) which = 1;
+    raft_msg_t m = {0};
+    if (which >= 0) {      /* take the head */
+      raft_msg_t* q = which ? rs : rq;
+      uint32_t* cnt = which ? &n->res_count : &n->req_count;
+      m = q[0];
+      memmove(q, q + 1, (*cnt - 1) * sizeof *q);
+      (*cnt)--;
+      memset(&q[*cnt], 0, sizeof *q);
+    }
+    raft_node_t nn = *n;
+    emit_t em[RAFT_MAX_NODES];
+    int ne = 0, fault = 0, elect = 0, mchg = 0;
+    uint32_t ev, msrc = 0, mterm = 0;
+    uint64_t appended = 0, applied = 0;
+    uint32_t type = m.hdr & 7, src = (m.hdr >> 3) & 15, flag = (m.hdr >> 7) & 1;
+    uint32_t pcnt = m.hdr >> 16;
+    if (which < 0) {
+      if (n->role == RAFT_LEADER) {                          /* heartbeat-handler 162-164 */
+        ev = 7;
+        fault = ae_broadcast(x, k, &nn, em, &ne);
+      } else {                                              /* timeout-handler 166-169 */
+        ev = 6;
+        nn.role = RAFT_CANDIDATE; nn.voted_for = (uint8_t)id;   /* follower->candidate 69-73 */
+        nn.votes = (uint16_t)(1u << id); nn.current_term = n->current_term + 1;
+        int present; raft_entry_t e;
+        fault = val_at(x, k, n->commit_index, &present, &e);  /* request-vote-rpc 48-54 */
+        if (!fault) {
+          for (uint32_t p = 1; p <= N; ++p) {
+            if (p == id) continue;
+            raft_msg_t r = {0};
+            r.term = nn.current_term; r.a = n->commit_index;
+            if (present) { r.eterm = e.term; r.eval = e.val; }
+            r.hdr = hdr(RAFT_MSG_REQUEST_VOTE, id, 0, present, 0);
+            em[ne].dst = p; em[ne].m = r; ne++;
+          }
+        }
+      }
+    } else {
+      ev = type; msrc = src; mterm = m.term;
+      raft_msg_t r = {0};
+      switch (type) {
+        case RAFT_MSG_REQUEST_VOTE: {                       /* request-vote-handler 91-103 */
+          int consistent = 1;
+          if (!(cfg->variant_flags & RAFT_VARIANT_VOTE_NO_LOG_CHECK))
+            fault = compare_prev(x, k, m.a, &m, &consistent);
+          if (fault) break;
+          int grant = m.term >= n->current_term && n->voted_for == 0 && consistent;
+          if (grant) nn.voted_for = (uint8_t)src;
+          r.term = n->current_term;
+          r.hdr = hdr(RAFT_MSG_VOTE_RESPONSE, id, (uint32_t)grant, 0, 0);
+          em[ne].dst = src; em[ne].m = r; ne++;
+          break;
+        }
+        case RAFT_MSG_APPEND_ENTRIES: {                     /* append-entries-handler 105-123 */
+          int consistent;
+          fault = compare_prev(x, k, m.b, &m, &consistent);
+          if (fault) break;
+          r.term = n->current_term;
+          if (m.term < n->current_term) {
+            r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 0, 0, 0);
+          } else if (!consistent) {
+            r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 0, 0, 0);
+            nn.log_len = n->log_len > m.b ? n->log_len - m.b : 0; /* remove-from! 78-81 */
+            nn.entries_is_seq = 1;
+          } else {
+            if (n->log_len + pcnt > s->L) { fault = RAFT_FAULT_OVERFLOW; break; }
+            plan[k].kind = PLAN_PAYLOAD; plan[k].src = src; plan[k].poff = m.poff;
+            plan[k].pcnt = pcnt;
+            plan_append(x, &nn, &plan[k], pcnt);                 /* append-entries! 61-64 */
+            appended = pcnt;
+            if (pcnt) appended_at[k] = (int)n->log_len;
+            uint32_t oldc = nn.commit_index;                        /* apply-entries! 69-76 */
+            nn.commit_index = nn.log_len;
+            applied = nn.commit_index > oldc ? nn.commit_index - oldc : 0;
+            r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 1, 0, 0);
+            r.a = m.a; r.b = m.b + pcnt;
+            nn.role = RAFT_FOLLWER; nn.voted_for = 0; nn.votes = 0; /* candidate->follower */
+            nn.leader_id = (uint8_t)src; nn.current_term = m.term;
+          }
+          em[ne].dst = src; em[ne].m = r; ne++;
+          break;
+        }
+        case RAFT_MSG_CLIENT_SET: {                          /* client-set-handler 151-160 */
+          if (n->role != RAFT_LEADER) break;                  /* redirect-client: no state */
+          if (n->log_len + 1 > s->L) { fault = RAFT_FAULT_OVERFLOW; break; }
+          plan[k].kind = PLAN_ENTRY;
+          plan[k].entry.term = n->current_term; plan[k].entry.val = m.a;
+          plan_append(x, &nn, &plan[k], 1);
+          appended = 1;
+          appended_at[k] = (int)n->log_len;
+          break;
+        }
+        case RAFT_MSG_VOTE_RESPONSE: {                       /* vote-response-handler 125-139 */
+          int present; raft_entry_t e;
+          fault = val_at(x, k, n->commit_index, &present, &e);     /* last-entry first */
+          if (fault) break;
+          if (m.term > n->current_term) {
+            nn.current_term = m.term;
+            nn.role = RAFT_FOLLWER; nn.voted_for = 0; nn.votes = 0;
+          } else if (!flag || n->role != RAFT_CANDIDATE) {
+          } else {
+            uint32_t votes = n->votes | (1u << src);
+            if (popcount16(votes) < (N + 1) / 2) {             /* majority? 19-21 */
+              nn.votes = (uint16_t)votes;
+            } else {
+              nn.role = RAFT_LEADER; nn.voted_for = 0; nn.votes = 0;   /* candidate->leader */
+              nn.leader_id = (uint8_t)id;
+              nn.ls_present = 1; nn.ls_keys = 0;                         /* leader-state 40-42 */
+              for (uint32_t p = 1; p <= N; ++p) {
+                nn.next_index[p - 1] = 0; nn.match_index[p - 1] = 0;
+                if (p == id) continue;
+                nn.ls_keys |= (uint16_t)(1u << p);
+                nn.next_index[p - 1] = (int32_t)(n->commit_index + 1);
+              }
+              fault = ae_broadcast(x, k, &nn, em, &ne);
+              elect = 1;
+            }
+          }
+          break;
+        }
+        case RAFT_MSG_APPEND_RESPONSE: {                     /* append-response-handler 141-149 */
+          if (m.term > n->current_term) {
+            nn.current_term = m.term;                        /* leader->follower 86-89 */
+            nn.role = RAFT_FOLLOWER; nn.leader_id = 0; nn.ls_present = 0; nn.ls_keys = 0;
+            memset(nn.next_index, 0, sizeof nn.next_index);
+            memset(nn.match_index, 0, sizeof nn.match_index);
+          } else if (!flag) {
+            if (!n->ls_present || !((n->ls_keys >> src) & 1)) { fault = RAFT_FAULT_NPE; break; }
+            nn.next_index[src - 1] -= 1;
+          } else {
+            nn.ls_present = 1;
+            nn.ls_keys |= (uint16_t)(1u << src);
+            nn.next_index[src - 1] = (int32_t)m.b;
+            nn.match_index[src - 1] = (int32_t)m.a;
+            mchg = 1;
+          }
+          break;
+        }
+        default:
+          break;
+      }
+    }
+    if (fault) {                                   /* D8: halted, pre-event state, no sends */
+      n->fault = (uint8_t)fault;
+      n->trace_hash = trace(n->trace_hash, t, ev, msrc, mterm, n, (uint32_t)fault);
+      lc->c[RAFT_CTR_HALT_IOOBE + fault - 1]++;
+      plan[k].kind = PLAN_NONE;
+      appended_at[k] = -1;
+      continue;
+    }
+    /* generate-timeout (core.clj:171-174) for the next wait */
+    nn.deadline = nn.role == RAFT_LEADER
+                      ? t + cfg->hb
+                      : t + cfg->el_base + (uint32_t)(((uint64_t)w[1] * cfg->el_span) >> 32);
+    nn.trace_hash = trace(n->trace_hash, t, ev, msrc, mterm, &nn, 0);
+    *n = nn;
+    lc->c[RAFT_CTR_EV_RV + ev - 1]++;
+    lc->c[RAFT_CTR_ENTRIES_APPENDED] += appended;
+    lc->c[RAFT_CTR_ENTRIES_APPLIED] += applied;
+    if (elect) {
+      lc->c[RAFT_CTR_LEADERS]++;
+      n->last_led_term = n->current_term;
+      elected |= 1u << k;
+    }
+    if (mchg) match_changed |= 1u << k;
+    for (int i = 0; i < ne; ++i) transmit(x, id, em[i].dst, &em[i].m);
+  }
+
+  /* P2 delivery: sender id ascending, copy 0 then 1 */
+  for (uint32_t r = 0; r < N; ++r)
+    for (uint32_t sd = 0; sd < N; ++sd) {
+      cell_t* cl = &x->cell[sd][r];
+      for (int i = 0; i < cl->n; ++i) {
+        raft_msg_t m = cl->m;
+        m.arrival = cl->arr[i];
+        queue_insert(x, r, &m);
+      }
+    }
+
+  /* P3 log writes (relocation + payload transfer) */
+  for (uint32_t k = 0; k < N; ++k) {
+    plan_t* pl = &plan[k];
+    if (pl->kind == PLAN_NONE) continue;
+    raft_node_t* n = &x->nodes[k];
+    raft_entry_t* ar = arena_of(s, c * N + k);
+    uint32_t m = pl->kind == PLAN_PAYLOAD ? pl->pcnt : 1;
+    if (m == 0) continue;
+    if (pl->reloc)
+      for (uint32_t i = 0; i < pl->old_len; ++i)
+        ar[(n->arena_base + i) % s->A] = ar[(pl->old_base + i) % s->A];
+    uint32_t dst = n->arena_base + pl->old_len;
+    if (pl->kind == PLAN_ENTRY) {
+      ar[dst % s->A] = pl->entry;
+    } else {
+      const raft_node_t* sn = &x->nodes[pl->src - 1];
+      const raft_entry_t* sa = arena_of(s, c * N + pl->src - 1);
+      for (uint32_t i = 0; i < m; ++i) {
+        raft_entry_t e = {0, 0};
+        if ((uint64_t)sn->arena_frontier > (uint64_t)pl->poff + i + s->A)
+          lc->c[RAFT_CTR_PAYLOAD_EVICTED]++;
+        else
+          e = sa[(pl->poff + i) % s->A];
+        ar[(dst + i) % s->A] = e;
+      }
+    }
+  }
+
+  /* P4 invariant checker */
+  if (elected || match_changed || 1) {
+    for (uint32_t k = 0; k < N; ++k) {
+      if (!((elected >> k) & 1)) continue;
+      uint32_t T = x->nodes[k].last_led_term;
+      for (uint32_t j = 0; j < N; ++j)
+        if (j != k && x->nodes[j].last_led_term == T) { violation(x, RAFT_CTR_VIOL_ELECTION); break; }
+    }
+    for (uint32_t k = 0; k < N; ++k) {
+      if (appended_at[k] < 0) continue;
+      const raft_node_t* nk = &x->nodes[k];
+      const raft_entry_t* ak = arena_of(s, c * N + k);
+      int bad = 0;
+      for (uint32_t j = 0; j < N && !bad; ++j) {
+        if (j == k) continue;
+        const raft_node_t* nj = &x->nodes[j];
+        const raft_entry_t* aj = arena_of(s, c * N + j);
+        uint32_t hi = nk->log_len < nj->log_len ? nk->log_len : nj->log_len;
+        for (uint32_t p = (uint32_t)appended_at[k]; p < hi; ++p) {
+          raft_entry_t a = ak[(nk->arena_base + p) % s->A], b = aj[(nj->arena_base + p) % s->A];
+          if (a.term == b.term && a.val != b.val) { bad = 1; break; }
+        }
+      }
+      if (bad) violation(x, RAFT_CTR_VIOL_LOG);
+    }
+    for (uint32_t k = 0; k < N; ++k) {
+      if (!((elected >> k) & 1) || hwm0.index == 0) continue;
+      const raft_node_t* nk = &x->nodes[k];
+      const raft_entry_t* ak = arena_of(s, c * N + k);
+      int ok = nk->log_len >= hwm0.index;
+      if (ok) {
+        raft_entry_t e = ak[(nk->arena_base + hwm0.index - 1) % s->A];
+        ok = e.term == hwm0.term && e.val == hwm0.val;
+      }
+      if (!ok) violation(x, RAFT_CTR_VIOL_COMPLETE);
+    }
+    int32_t best = -1;
+    raft_hwm_t nh = s->hwm[c];
+    for (uint32_t k = 0; k < N; ++k) {
+      const raft_node_t* nk = &x->nodes[k];
+      if (nk->role != RAFT_LEADER || !(((elected | match_changed) >> k) & 1)) continue;
+      int32_t vals[RAFT_MAX_NODES];
+      uint32_t nv = 0;
+      vals[nv++] = (int32_t)nk->log_len;
+      for (uint32_t p = 1; p <= N; ++p)
+        if (p != k + 1) vals[nv++] = ((nk->ls_keys >> p) & 1) ? nk->match_index[p - 1] : 0;
+      for (uint32_t i = 1; i < nv; ++i)       /* sort descending */
+        for (uint32_t j = i; j > 0 && vals[j - 1] < vals[j]; --j) {
+          int32_t tmp = vals[j]; vals[j] = vals[j - 1]; vals[j - 1] = tmp;
+        }
+      int32_t mm = vals[(N + 1) / 2 - 1];
+      if (mm > (int32_t)nk->log_len) mm = (int32_t)nk->log_len;
+      if (mm > (int32_t)s->hwm[c].index && mm > best) {
+        best = mm;
+        raft_entry_t e = arena_of(s, c * N + k)[(nk->arena_base + (uint32_t)mm - 1) % s->A];
+        nh.index = (uint32_t)mm; nh.term = e.term; nh.val = e.val;
+      }
+    }
+    if (best > 0) s->hwm[c] = nh;
+  }
+}
+
+/* ---------------------------------------------------------------- stepping (pmap over chunks) */
+typedef struct {
+  raft_ref_t* s;
+  uint32_t c0, c1, t0, n;
+  local_ctr_t lc;
+} job_t;
+
+static void* run_job(void* arg) {
+  job_t* j = (job_t*)arg;
+  memset(&j->lc, 0, sizeof j->lc);
+  j->lc.first_violation = UINT64_MAX;
+  for (uint32_t c = j->c0; c < j->c1; ++c)
+    for (uint32_t i = 0; i < j->n; ++i) step_cluster(j->s, c, j->t0 + i, &j->lc);
+  return NULL;
+}
+
+int raft_ref_step(raft_ref_t* s, uint32_t n_ticks) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if (s->tick + n_ticks > 0xFFFFFFFFull) return fail(-EINVAL, "tick counter would exceed 2^32");
+  int T = s->threads;
+  if ((uint32_t)T > s->C) T = (int)s->C;
+  job_t* jobs = (job_t*)calloc((size_t)T, sizeof *jobs);
+  pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof *th);
+  if (!jobs || !th) { free(jobs); free(th); return fail(-ENOMEM, "oom"); }
+  for (int i = 0; i < T; ++i) {
+    jobs[i].s = s; jobs[i].t0 = (uint32_t)s->tick; jobs[i].n = n_ticks;
+    jobs[i].c0 = (uint32_t)((uint64_t)s->C * i / T);
+    jobs[i].c1 = (uint32_t)((uint64_t)s->C * (i + 1) / T);
+  }
+  if (T == 1) {
+    run_job(&jobs[0]);
+  } else {
+    for (int i = 0; i < T; ++i) pthread_create(&th[i], NULL, run_job, &jobs[i]);
+    for (int i = 0; i < T; ++i) pthread_join(th[i], NULL);
+  }
+  for (int i = 0; i < T; ++i) {
+    for (int k = 0; k < RAFT_CTR_COUNT; ++k) s->ctr.c[k] += jobs[i].lc.c[k];
+    if (jobs[i].lc.first_violation < s->ctr.first_violation_tick)
+      s->ctr.first_violation_tick = jobs[i].lc.first_violation;
+  }
+  s->ctr.node_ticks += (uint64_t)s->C * s->N * n_ticks;
+  s->tick += n_ticks;
+  free(jobs); free(th);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- state access */
+static int check_range(raft_ref_t* s, uint32_t c0, uint32_t nc) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if ((uint64_t)c0 + nc > s->C) return fail(-EINVAL, "cluster range out of bounds");
+  return 0;
+}
+static int check_node(raft_ref_t* s, uint32_t cluster, uint32_t id) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
+  return 0;
+}
+
+int raft_ref_read_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  memcpy(out, s->nodes + (size_t)c0 * s->N, (size_t)nc * s->N * sizeof(raft_node_t));
+  return 0;
+}
+
+int raft_ref_write_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  const uint32_t N = s->N, all = ((1u << (N + 1)) - 1) & ~1u;
+  for (size_t i = 0; i < (size_t)nc * N; ++i) {
+    const raft_node_t* n = &in[i];
+    uint32_t id = (uint32_t)(i % N) + 1, peers = all & ~(1u << id);
+    if (n->role > 3 || n->voted_for > N || n->leader_id > N || n->fault > 4 ||
+        (n->votes & ~all) || (n->ls_keys & ~peers) || n->entries_is_seq > 1 || n->ls_present > 1 ||
+        n->log_len > s->L || n->arena_frontier - n->arena_base < n->log_len ||
+        n->arena_frontier - n->arena_base > s->L ||
+        (n->role == RAFT_LEADER && (!n->ls_present || n->ls_keys != peers)) ||
+        (!n->ls_present && n->ls_keys))
+      return fail(-EINVAL, "invalid node record");
+  }
+  for (size_t i = 0; i < (size_t)nc * N; ++i) {
+    raft_node_t* d = &s->nodes[(size_t)c0 * N + i];
+    uint32_t rq = d->req_count, rs = d->res_count;
+    *d = in[i];
+    d->req_count = rq; d->res_count = rs;
+    d->reserved0 = 0; d->reserved1 = 0;
+    for (uint32_t p = N; p < RAFT_MAX_NODES; ++p) { d->next_index[p] = 0; d->match_index[p] = 0; }
+  }
+  return 0;
+}
+
+int raft_ref_read_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+                        raft_msg_t* out, uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (which > 1) return fail(-EINVAL, "which must be 0 (req) or 1 (res)");
+  raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
+  uint32_t cnt = which ? n->res_count : n->req_count;
+  uint32_t m = cnt < cap ? cnt : cap;
+  memcpy(out, qslot(s, cluster * s->N + id - 1, (int)which), m * sizeof(raft_msg_t));
+  return (int)cnt;
+}
+
+int raft_ref_write_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+                         const raft_msg_t* in, uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (which > 1 || count > s->Q) return fail(-EINVAL, "bad queue or count");
+  for (uint32_t i = 0; i < count; ++i) {
+    uint32_t type = in[i].hdr & 7, src = (in[i].hdr >> 3) & 15;
+    int want = type <= RAFT_MSG_CLIENT_SET ? 0 : 1;
+    if (type < 1 || type > 5 || want != (int)which || src > s->N || src == id ||
+        (type == RAFT_MSG_CLIENT_SET) != (src == 0) ||
+        (i > 0 && in[i].arrival < in[i - 1].arrival))
+      return fail(-EINVAL, "invalid message or order");
+  }
+  raft_msg_t* q = qslot(s, cluster * s->N + id - 1, (int)which);
+  memset(q, 0, s->Q * sizeof *q);
+  memcpy(q, in, count * sizeof *q);
+  raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
+  if (which) n->res_count = count; else n->req_count = count;
+  return 0;
+}
+
+int raft_ref_read_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
+                        uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  uint32_t m = cap < s->A ? cap : s->A;
+  memcpy(out, arena_of(s, cluster * s->N + id - 1), m * sizeof(raft_entry_t));
+  return (int)s->A;
+}
+
+int raft_ref_write_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+                         uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (count > s->A) return fail(-EINVAL, "count > arena_cap");
+  raft_entry_t* a = arena_of(s, cluster * s->N + id - 1);
+  memset(a, 0, s->A * sizeof *a);
+  memcpy(a, in, count * sizeof *a);
+  return 0;
+}
+
+int raft_ref_read_hwm(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_hwm_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  memcpy(out, s->hwm + c0, nc * sizeof *out);
+  return 0;
+}
+
+int raft_ref_write_hwm(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_hwm_t* in) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  memcpy(s->hwm + c0, in, nc * sizeof *in);
+  for (uint32_t i = 0; i < nc; ++i) s->hwm[c0 + i].reserved = 0;
+  return 0;
+}
+
+int raft_ref_read_counters(raft_ref_t* s, raft_counters_t* out) {
+  if (!s || !out) return fail(-EINVAL, "null argument");
+  *out = s->ctr;
+  return 0;
+}
+
+int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  const uint32_t N = s->N;
+  for (uint32_t ci = 0; ci < nc; ++ci) {
+    uint32_t c = c0 + ci;
+    uint64_t h = FNV_OFFSET;
+    for (uint32_t k = 0; k < N; ++k) {
+      const raft_node_t* n = &s->nodes[(size_t)c * N + k];
+      uint32_t hdrw[12] = {n->role, n->voted_for, n->leader_id, n->fault, n->entries_is_seq,
+                           n->ls_present, n->votes, n->ls_keys, n->current_term,
+                           n->commit_index, n->log_len, n->deadline};
+      for (int i = 0; i < 12; ++i) h = fnv(h, hdrw[i]);
+      for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)n->next_index[p]);
+      for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)n->match_index[p]);
+      h = fnv(h, n->last_led_term);
+      h = fnv(h, (uint32_t)n->trace_hash);
+      h = fnv(h, (uint32_t)(n->trace_hash >> 32));
+      h = fnv(h, n->arena_base);
+      h = fnv(h, n->arena_frontier);
+      for (int which = 0; which < 2; ++which) {
+        uint32_t cnt = which ? n->res_count : n->req_count;
+        h = fnv(h, cnt);
+        const raft_msg_t* q = qslot(s, c * N + k, which);
+        for (uint32_t i = 0; i < cnt; ++i) {
+          const uint32_t* wds = (const uint32_t*)&q[i];
+          for (int j = 0; j < 8; ++j) h = fnv(h, wds[j]);
+        }
+      }
+      const raft_entry_t* a = arena_of(s, c * N + k);
+      for (uint32_t i = 0; i < n->log_len; ++i) {
+        raft_entry_t e = a[(n->arena_base + i) % s->A];
+        h = fnv(h, e.term);
+        h = fnv(h, e.val);
+      }
+    }
+    h = fnv(h, s->hwm[c].index);
+    h = fnv(h, s->hwm[c].term);
+    h = fnv(h, s->hwm[c].val);
+    out[ci] = h;
+  }
+  return 0;
+}
+
+int raft_ref_abi_version(void) { return RAFT_SIM_ABI_VERSION; }

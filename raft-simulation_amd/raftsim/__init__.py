@@ -1,0 +1,26 @@
+"""raftsim — host side of the MI355X batched Raft simulator (libraftsim.so).
+
+`Simulator` is the drop-in for the reference's per-process node loop (`-main`/`wait`,
+src/raft/core.clj:176-203): it advances `n_clusters` independent N-node clusters in lockstep on one
+GPU through the C ABI of include/raftsim.h. There is no CPU fallback: if libraftsim.so is missing
+or was not built for this machine, construction raises.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+from ._abi import COUNTER_NAMES  # noqa: F401
+from ._backend import FAULT_NAMES, ROLE_NAMES, Backend, RaftSimError  # noqa: F401
+
+PKG_DIR = Path(__file__).resolve().parent.parent          # raft-simulation_amd/
+LIB_PATH = Path(os.environ.get("RAFTSIM_LIB", PKG_DIR / "build" / "libraftsim.so"))
+
+
+class Simulator(Backend):
+    """Batched simulator on the GPU (HIP kernels for gfx950)."""
+
+    def __init__(self, **config):
+        if not LIB_PATH.exists():
+            raise RaftSimError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+        super().__init__(LIB_PATH, "raft_sim_", **config)
