@@ -1,0 +1,160 @@
+// device.hpp — device-side building blocks of the tick kernel (gfx950 / CDNA4).
+//
+// Layout in HBM (structure of arrays, node index gi = cluster * N + k, k = id - 1):
+//   hot node words   flags, masks, term, commit, len, deadline, qmeta, req/res head+tail arrival,
+//                    arena base/frontier, last_led, trace lo/hi           [NN] u32 each
+//   cold node words  next_index / match_index                              [N][NN] i32
+//   queues           qbuf[gi][which][Q] of 8-word messages (ring, sorted by arrival)
+//   log arenas       arena[gi][A] of (term, val)
+//   cluster words    hwm[c] = (index, term, val, 0)
+// A wave owns floor(64 / N) whole clusters, one lane per node; a cluster never spans waves, so all
+// intra-cluster traffic is lane-to-lane inside one wave (LDS cells + ds_bpermute).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/raftsim.h"
+
+namespace rs {
+
+constexpr uint32_t INF = 0xFFFFFFFFu;
+enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_CLIENT_DETAIL = 5, P_PART = 6 };
+enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
+constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;  // per-wave LDS counter slot holding min tick
+constexpr int LCTR_WORDS = 32;
+
+struct DevSim {
+  uint32_t C, N, Q, L, A, NN, goff, key0, key1;
+  uint32_t hb, el_base, el_span, drop_ppm, dup_ppm, dmin, dmax, part_ppm, part_epoch,
+      client_ppm, variant;
+  uint32_t *flags, *masks, *term, *commit, *len, *deadline, *qmeta, *req_arr, *res_arr,
+      *req_tail, *res_tail, *abase, *afront, *led, *trace_lo, *trace_hi;
+  int32_t *next, *match;  // [N][NN], row p-1 for peer id p
+  uint32_t* qbuf;         // [NN][2][Q][8]
+  uint32_t* arena;        // [NN][A][2]
+  uint32_t* hwm;          // [C][4]
+  unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)
+};
+
+// Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).
+__device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ uint32_t ppm(uint32_t w) { return __umulhi(w, 1000000u); }
+
+__device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
+  return (h ^ w) * 0x100000001B3ull;
+}
+
+// Flags word: role 0-1 | voted_for 2-5 | leader_id 6-9 | fault 10-12 | is_seq 13 | ls_present 14
+__host__ __device__ __forceinline__ uint32_t pack_flags(uint32_t role, uint32_t vf, uint32_t lid,
+                                                        uint32_t fault, uint32_t seq,
+                                                        uint32_t lsp) {
+  return role | vf << 2 | lid << 6 | fault << 10 | seq << 13 | lsp << 14;
+}
+// qmeta: req_head 0-3 | req_cnt 4-8 | res_head 9-12 | res_cnt 13-17
+__host__ __device__ __forceinline__ uint32_t pack_qmeta(uint32_t rqh, uint32_t rqc, uint32_t rsh,
+                                                        uint32_t rsc) {
+  return rqh | rqc << 4 | rsh << 9 | rsc << 13;
+}
+
+// One queue's registers: ring head, count, head arrival (INF when empty), tail arrival.
+struct QueueR {
+  uint32_t h, c, arr, tail;
+};
+
+// Node registers held by one lane for a whole launch. Queues are named fields (never indexed by a
+// runtime value) so that they stay in VGPRs.
+struct NodeR {
+  uint32_t role, vf, lid, fault, seq, lsp, votes, keys;
+  uint32_t term, commit, len, deadline;
+  QueueR rq, rs;
+  uint32_t base, front, led;
+  uint64_t trace;
+};
+
+__device__ __forceinline__ uint32_t wrapq(uint32_t x, uint32_t Q) { return x >= Q ? x - Q : x; }
+
+__device__ __forceinline__ uint32_t* qslots(const DevSim& S, uint32_t gi, int which) {
+  return S.qbuf + ((size_t)gi * 2 + which) * S.Q * 8;
+}
+
+__device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
+  return reinterpret_cast<uint2*>(S.arena) + (size_t)gi * S.A;
+}
+
+__device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
+  if (v) atomicAdd(&lctr[i], v);
+}
+
+// Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own
+// queue `which` (SIM_SPEC §4 P2: after every queued message whose arrival <= the new one).
+__device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
+                                        QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr) {
+  if (fault) {
+    lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
+    return;
+  }
+  const uint32_t Q = S.Q;
+  if (q.c >= Q) {
+    lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
+    return;
+  }
+  uint32_t* qb = qslots(S, gi, which);
+  const uint32_t arr = m0.x, head = q.h;
+  uint32_t pos = q.c;
+  if (pos > 0 && arr < q.tail) {
+    while (pos > 0) {
+      const uint32_t prev = wrapq(head + pos - 1, Q);
+      if (qb[prev * 8] <= arr) break;
+      const uint32_t dst = wrapq(head + pos, Q);
+      uint4* sp = reinterpret_cast<uint4*>(qb + prev * 8);
+      uint4* dp = reinterpret_cast<uint4*>(qb + dst * 8);
+      dp[0] = sp[0];
+      dp[1] = sp[1];
+      --pos;
+    }
+  } else {
+    q.tail = arr;
+  }
+  uint4* dp = reinterpret_cast<uint4*>(qb + wrapq(head + pos, Q) * 8);
+  dp[0] = m0;
+  dp[1] = m1;
+  q.c += 1;
+  if (pos == 0) q.arr = arr;
+  lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+}
+
+// Take the head of queue `which`.
+__device__ __forceinline__ void qpop(const DevSim& S, uint32_t gi, int which, QueueR& q, uint4& m0,
+                                     uint4& m1) {
+  uint32_t* qb = qslots(S, gi, which);
+  const uint32_t head = q.h;
+  const uint4* sp = reinterpret_cast<const uint4*>(qb + head * 8);
+  m0 = sp[0];
+  m1 = sp[1];
+  const uint32_t nh = wrapq(head + 1, S.Q);
+  q.h = nh;
+  q.c -= 1;
+  if (q.c) {
+    q.arr = qb[nh * 8];
+  } else {
+    q.arr = INF;
+    q.tail = 0;
+  }
+}
+
+}  // namespace rs

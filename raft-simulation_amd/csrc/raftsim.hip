@@ -1,0 +1,432 @@
+// raftsim.hip — C ABI of libraftsim.so (include/raftsim.h) over the gfx950 tick kernel.
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "device.hpp"
+
+namespace rs {
+hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st);
+hipError_t launch_init(const DevSim& S, hipStream_t st);
+hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
+                         hipStream_t st);
+hipError_t configure_kernels();
+}  // namespace rs
+
+using rs::DevSim;
+
+static thread_local char g_err[512];
+
+static int fail(int code, const char* fmt, const char* detail = "") {
+  snprintf(g_err, sizeof g_err, fmt, detail);
+  return code;
+}
+
+#define HIP_OK(expr)                                                               \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) return fail(-EIO, "HIP error: %s (" #expr ")",           \
+                                      hipGetErrorString(e_));                      \
+  } while (0)
+
+struct raft_sim {
+  raft_sim_config_t cfg;
+  uint32_t N, Q, L, A, C, NN, tpl;
+  uint64_t tick;
+  hipStream_t stream;
+  hipEvent_t ev_start, ev_stop;
+  DevSim d;
+  std::vector<void*> allocs;
+  double last_ms;
+  uint32_t last_launches;
+};
+
+// Exported functions take their C linkage from the declarations in include/raftsim.h.
+
+const char* raft_sim_last_error(void) { return g_err; }
+int raft_sim_abi_version(void) { return RAFT_SIM_ABI_VERSION; }
+
+void raft_sim_default_config(raft_sim_config_t* c) {
+  memset(c, 0, sizeof *c);
+  c->n_clusters = 1; c->nodes = 5; c->log_cap = 64; c->inbox_cap = 16; c->seed = 42;
+  c->hb = 3000; c->el_base = 5000; c->el_span = 5000; c->dmin = 1; c->dmax = 1;
+  c->part_epoch = 1000;
+}
+
+static int validate_cfg(const raft_sim_config_t* c) {
+  if (c->nodes < 2 || c->nodes > RAFT_MAX_NODES) return fail(-EINVAL, "nodes must be 2..9");
+  if (c->n_clusters == 0) return fail(-EINVAL, "n_clusters must be > 0");
+  if ((uint64_t)c->n_clusters * c->nodes > 0x7FFFFFFFull) return fail(-EINVAL, "too many nodes");
+  if (c->inbox_cap < 1 || c->inbox_cap > RAFT_MAX_INBOX) return fail(-EINVAL, "inbox_cap 1..16");
+  if (c->log_cap < 1 || c->log_cap > 65535) return fail(-EINVAL, "log_cap 1..65535");
+  uint64_t A = c->arena_cap ? c->arena_cap : 4ull * c->log_cap;
+  if (A < 2ull * c->log_cap || A > (1u << 24))
+    return fail(-EINVAL, "arena_cap must be >= 2*log_cap");
+  if (c->hb < 1 || c->el_base < 1) return fail(-EINVAL, "hb and el_base must be >= 1");
+  if (c->dmin < 1 || c->dmax < c->dmin || c->dmax > 255)
+    return fail(-EINVAL, "1 <= dmin <= dmax <= 255");
+  if (c->part_epoch < 1) return fail(-EINVAL, "part_epoch must be >= 1");
+  if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
+      c->client_ppm > 1000000)
+    return fail(-EINVAL, "ppm values must be <= 1e6");
+  return 0;
+}
+
+template <typename T>
+static int dalloc(raft_sim* s, T** p, size_t count) {
+  void* v = nullptr;
+  hipError_t e = hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T));
+  if (e != hipSuccess) return fail(-ENOMEM, "hipMalloc failed: %s", hipGetErrorString(e));
+  s->allocs.push_back(v);
+  *p = static_cast<T*>(v);
+  return 0;
+}
+
+void raft_sim_destroy(raft_sim_t* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->cfg.device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* p : s->allocs) (void)hipFree(p);
+  if (s->ev_start) (void)hipEventDestroy(s->ev_start);
+  if (s->ev_stop) (void)hipEventDestroy(s->ev_stop);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
+  if (!cfg || !out) return fail(-EINVAL, "null argument");
+  int rc = validate_cfg(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(-EIO, "no HIP device visible: libraftsim.so requires an MI355X (gfx950)");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(-EINVAL, "device ordinal out of range");
+  HIP_OK(hipSetDevice(cfg->device));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, cfg->device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(-EIO, "device is %s; libraftsim.so is built for gfx950", prop.gcnArchName);
+  HIP_OK(rs::configure_kernels());
+
+  raft_sim* s = new raft_sim();
+  s->cfg = *cfg;
+  s->N = cfg->nodes; s->Q = cfg->inbox_cap; s->L = cfg->log_cap; s->C = cfg->n_clusters;
+  s->A = cfg->arena_cap ? cfg->arena_cap : 4 * cfg->log_cap;
+  s->NN = s->C * s->N;
+  s->tpl = cfg->ticks_per_launch ? std::min<uint32_t>(cfg->ticks_per_launch, 65536u) : 10000u;
+  DevSim& d = s->d;
+  d.C = s->C; d.N = s->N; d.Q = s->Q; d.L = s->L; d.A = s->A; d.NN = s->NN;
+  d.goff = cfg->cluster_offset;
+  d.key0 = (uint32_t)cfg->seed; d.key1 = (uint32_t)(cfg->seed >> 32);
+  d.hb = cfg->hb; d.el_base = cfg->el_base; d.el_span = cfg->el_span;
+  d.drop_ppm = cfg->drop_ppm; d.dup_ppm = cfg->dup_ppm; d.dmin = cfg->dmin; d.dmax = cfg->dmax;
+  d.part_ppm = cfg->part_ppm; d.part_epoch = cfg->part_epoch; d.client_ppm = cfg->client_ppm;
+  d.variant = cfg->variant_flags;
+  const size_t NN = s->NN;
+  uint32_t** hot[] = {&d.flags, &d.masks, &d.term, &d.commit, &d.len, &d.deadline, &d.qmeta,
+                      &d.req_arr, &d.res_arr, &d.req_tail, &d.res_tail, &d.abase, &d.afront,
+                      &d.led, &d.trace_lo, &d.trace_hi};
+  for (uint32_t** p : hot)
+    if ((rc = dalloc(s, p, NN))) { raft_sim_destroy(s); return rc; }
+  if ((rc = dalloc(s, &d.next, NN * s->N)) || (rc = dalloc(s, &d.match, NN * s->N)) ||
+      (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
+      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.hwm, (size_t)s->C * 4)) ||
+      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1))) {
+    raft_sim_destroy(s);
+    return rc;
+  }
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreate(&s->ev_start)) != hipSuccess ||
+      (e = hipEventCreate(&s->ev_stop)) != hipSuccess ||
+      (e = hipMemsetAsync(d.next, 0, NN * s->N * 4, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.match, 0, NN * s->N * 4, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.hwm, 0, (size_t)s->C * 16, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
+      (e = rs::launch_init(d, s->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
+    raft_sim_destroy(s);
+    return fail(-EIO, "HIP error during create: %s", hipGetErrorString(e));
+  }
+  *out = s;
+  return 0;
+}
+
+int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if (s->tick + n_ticks > 0xFFFFFFFFull) return fail(-EINVAL, "tick counter would exceed 2^32");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  uint32_t launches = 0;
+  HIP_OK(hipEventRecord(s->ev_start, s->stream));
+  for (uint32_t done = 0; done < n_ticks;) {
+    const uint32_t nt = std::min(s->tpl, n_ticks - done);
+    HIP_OK(rs::launch_tick(s->d, (uint32_t)s->tick + done, nt, s->stream));
+    done += nt;
+    ++launches;
+  }
+  HIP_OK(hipEventRecord(s->ev_stop, s->stream));
+  HIP_OK(hipEventSynchronize(s->ev_stop));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, s->ev_start, s->ev_stop));
+  s->last_ms = launches ? ms / launches : 0.0;
+  s->last_launches = launches;
+  s->tick += n_ticks;
+  return 0;
+}
+
+int raft_sim_last_step_timing(raft_sim_t* s, double* avg_kernel_ms, uint32_t* launches) {
+  if (!s || !avg_kernel_ms || !launches) return fail(-EINVAL, "null argument");
+  *avg_kernel_ms = s->last_ms;
+  *launches = s->last_launches;
+  return 0;
+}
+
+uint64_t raft_sim_tick(const raft_sim_t* s) { return s ? s->tick : 0; }
+
+static int check_range(raft_sim* s, uint32_t c0, uint32_t nc) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if ((uint64_t)c0 + nc > s->C) return fail(-EINVAL, "cluster range out of bounds");
+  return 0;
+}
+
+static int check_node(raft_sim* s, uint32_t cluster, uint32_t id) {
+  if (!s) return fail(-EINVAL, "null sim");
+  if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
+  return 0;
+}
+
+template <typename T>
+static hipError_t d2h(raft_sim* s, T* host, const T* dev, size_t count) {
+  return hipMemcpyAsync(host, dev, count * sizeof(T), hipMemcpyDeviceToHost, s->stream);
+}
+template <typename T>
+static hipError_t h2d(raft_sim* s, T* dev, const T* host, size_t count) {
+  return hipMemcpyAsync(dev, host, count * sizeof(T), hipMemcpyHostToDevice, s->stream);
+}
+
+int raft_sim_read_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  if (!out) return fail(-EINVAL, "null output");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const size_t n0 = (size_t)c0 * s->N, cnt = (size_t)nc * s->N, NN = s->NN, N = s->N;
+  std::vector<uint32_t> w(16 * cnt);
+  std::vector<int32_t> nx(N * cnt), mt(N * cnt);
+  const DevSim& d = s->d;
+  const uint32_t* src[16] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.qmeta,
+                             d.req_arr, d.res_arr, d.req_tail, d.res_tail, d.abase, d.afront,
+                             d.led, d.trace_lo, d.trace_hi};
+  for (int f = 0; f < 16; ++f) HIP_OK(d2h(s, &w[f * cnt], src[f] + n0, cnt));
+  for (size_t p = 0; p < N; ++p) {
+    HIP_OK(d2h(s, &nx[p * cnt], d.next + p * NN + n0, cnt));
+    HIP_OK(d2h(s, &mt[p * cnt], d.match + p * NN + n0, cnt));
+  }
+  HIP_OK(hipStreamSynchronize(s->stream));
+  for (size_t i = 0; i < cnt; ++i) {
+    raft_node_t& r = out[i];
+    memset(&r, 0, sizeof r);
+    const uint32_t fl = w[i], mk = w[cnt + i], qm = w[6 * cnt + i];
+    r.role = fl & 3; r.voted_for = (fl >> 2) & 15; r.leader_id = (fl >> 6) & 15;
+    r.fault = (fl >> 10) & 7; r.entries_is_seq = (fl >> 13) & 1; r.ls_present = (fl >> 14) & 1;
+    r.votes = mk & 0xFFFF; r.ls_keys = mk >> 16;
+    r.current_term = w[2 * cnt + i]; r.commit_index = w[3 * cnt + i];
+    r.log_len = w[4 * cnt + i]; r.deadline = w[5 * cnt + i];
+    for (size_t p = 0; p < N; ++p) {
+      r.next_index[p] = nx[p * cnt + i];
+      r.match_index[p] = mt[p * cnt + i];
+    }
+    r.last_led_term = w[13 * cnt + i];
+    r.arena_base = w[11 * cnt + i]; r.arena_frontier = w[12 * cnt + i];
+    r.req_count = (qm >> 4) & 31; r.res_count = (qm >> 13) & 31;
+    r.trace_hash = (uint64_t)w[15 * cnt + i] << 32 | w[14 * cnt + i];
+  }
+  return 0;
+}
+
+int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  if (!in) return fail(-EINVAL, "null input");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const uint32_t N = s->N, all = ((1u << (N + 1)) - 1) & ~1u;
+  const size_t n0 = (size_t)c0 * N, cnt = (size_t)nc * N, NN = s->NN;
+  for (size_t i = 0; i < cnt; ++i) {
+    const raft_node_t* n = &in[i];
+    uint32_t id = (uint32_t)(i % N) + 1, peers = all & ~(1u << id);
+    if (n->role > 3 || n->voted_for > N || n->leader_id > N || n->fault > 4 ||
+        (n->votes & ~all) || (n->ls_keys & ~peers) || n->entries_is_seq > 1 ||
+        n->ls_present > 1 || n->log_len > s->L ||
+        n->arena_frontier - n->arena_base < n->log_len ||
+        n->arena_frontier - n->arena_base > s->L ||
+        (n->role == RAFT_LEADER && (!n->ls_present || n->ls_keys != peers)) ||
+        (!n->ls_present && n->ls_keys))
+      return fail(-EINVAL, "invalid node record");
+  }
+  std::vector<uint32_t> w(14 * cnt);
+  std::vector<int32_t> nx(N * cnt), mt(N * cnt);
+  for (size_t i = 0; i < cnt; ++i) {
+    const raft_node_t& r = in[i];
+    w[i] = rs::pack_flags(r.role, r.voted_for, r.leader_id, r.fault, r.entries_is_seq,
+                          r.ls_present);
+    w[cnt + i] = r.votes | (uint32_t)r.ls_keys << 16;
+    w[2 * cnt + i] = r.current_term; w[3 * cnt + i] = r.commit_index;
+    w[4 * cnt + i] = r.log_len; w[5 * cnt + i] = r.deadline;
+    w[6 * cnt + i] = r.arena_base; w[7 * cnt + i] = r.arena_frontier;
+    w[8 * cnt + i] = r.last_led_term;
+    w[9 * cnt + i] = (uint32_t)r.trace_hash; w[10 * cnt + i] = (uint32_t)(r.trace_hash >> 32);
+    for (size_t p = 0; p < N; ++p) {
+      nx[p * cnt + i] = r.next_index[p];
+      mt[p * cnt + i] = r.match_index[p];
+    }
+  }
+  const DevSim& d = s->d;
+  uint32_t* dst[11] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.abase,
+                       d.afront, d.led, d.trace_lo, d.trace_hi};
+  for (int f = 0; f < 11; ++f) HIP_OK(h2d(s, dst[f] + n0, &w[f * cnt], cnt));
+  for (size_t p = 0; p < N; ++p) {
+    HIP_OK(h2d(s, d.next + p * NN + n0, &nx[p * cnt], cnt));
+    HIP_OK(h2d(s, d.match + p * NN + n0, &mt[p * cnt], cnt));
+  }
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_read_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+                        raft_msg_t* out, uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (which > 1) return fail(-EINVAL, "which must be 0 (req) or 1 (res)");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const uint32_t gi = cluster * s->N + id - 1;
+  uint32_t qm = 0;
+  std::vector<raft_msg_t> slots(s->Q);
+  HIP_OK(d2h(s, &qm, s->d.qmeta + gi, 1));
+  HIP_OK(hipMemcpyAsync(slots.data(), s->d.qbuf + ((size_t)gi * 2 + which) * s->Q * 8,
+                        s->Q * sizeof(raft_msg_t), hipMemcpyDeviceToHost, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  const uint32_t head = which ? (qm >> 9) & 15 : qm & 15;
+  const uint32_t cnt = which ? (qm >> 13) & 31 : (qm >> 4) & 31;
+  for (uint32_t i = 0; i < cnt && i < cap && out; ++i) out[i] = slots[(head + i) % s->Q];
+  return (int)cnt;
+}
+
+int raft_sim_write_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+                         const raft_msg_t* in, uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (which > 1 || count > s->Q || (count && !in)) return fail(-EINVAL, "bad queue or count");
+  for (uint32_t i = 0; i < count; ++i) {
+    uint32_t type = in[i].hdr & 7, src = (in[i].hdr >> 3) & 15;
+    int want = type <= RAFT_MSG_CLIENT_SET ? 0 : 1;
+    if (type < 1 || type > 5 || want != (int)which || src > s->N || src == id ||
+        (type == RAFT_MSG_CLIENT_SET) != (src == 0) ||
+        (i > 0 && in[i].arrival < in[i - 1].arrival))
+      return fail(-EINVAL, "invalid message or order");
+  }
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const uint32_t gi = cluster * s->N + id - 1;
+  std::vector<raft_msg_t> slots(s->Q);
+  memset(slots.data(), 0, s->Q * sizeof(raft_msg_t));
+  for (uint32_t i = 0; i < count; ++i) slots[i] = in[i];
+  uint32_t qm = 0;
+  HIP_OK(d2h(s, &qm, s->d.qmeta + gi, 1));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  if (which) qm = (qm & ~(0xFu << 9 | 0x1Fu << 13)) | count << 13;
+  else qm = (qm & ~0x1FFu) | count << 4;
+  const uint32_t harr = count ? in[0].arrival : rs::INF, tail = count ? in[count - 1].arrival : 0;
+  HIP_OK(hipMemcpyAsync(s->d.qbuf + ((size_t)gi * 2 + which) * s->Q * 8, slots.data(),
+                        s->Q * sizeof(raft_msg_t), hipMemcpyHostToDevice, s->stream));
+  HIP_OK(h2d(s, s->d.qmeta + gi, &qm, 1));
+  HIP_OK(h2d(s, (which ? s->d.res_arr : s->d.req_arr) + gi, &harr, 1));
+  HIP_OK(h2d(s, (which ? s->d.res_tail : s->d.req_tail) + gi, &tail, 1));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_read_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
+                        uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (out && cap) {
+    HIP_OK(hipSetDevice(s->cfg.device));
+    const size_t gi = (size_t)cluster * s->N + id - 1;
+    HIP_OK(hipMemcpyAsync(out, s->d.arena + gi * s->A * 2,
+                          std::min(cap, s->A) * sizeof(raft_entry_t), hipMemcpyDeviceToHost,
+                          s->stream));
+    HIP_OK(hipStreamSynchronize(s->stream));
+  }
+  return (int)s->A;
+}
+
+int raft_sim_write_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+                         uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (count > s->A || (count && !in)) return fail(-EINVAL, "count > arena_cap");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  std::vector<raft_entry_t> buf(s->A);
+  memset(buf.data(), 0, s->A * sizeof(raft_entry_t));
+  if (count) memcpy(buf.data(), in, count * sizeof(raft_entry_t));
+  const size_t gi = (size_t)cluster * s->N + id - 1;
+  HIP_OK(hipMemcpyAsync(s->d.arena + gi * s->A * 2, buf.data(), s->A * sizeof(raft_entry_t),
+                        hipMemcpyHostToDevice, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_read_hwm(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_hwm_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  HIP_OK(hipMemcpyAsync(out, s->d.hwm + (size_t)c0 * 4, nc * sizeof(raft_hwm_t),
+                        hipMemcpyDeviceToHost, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_write_hwm(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_hwm_t* in) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  std::vector<raft_hwm_t> buf(in, in + nc);
+  for (auto& h : buf) h.reserved = 0;
+  HIP_OK(hipMemcpyAsync(s->d.hwm + (size_t)c0 * 4, buf.data(), nc * sizeof(raft_hwm_t),
+                        hipMemcpyHostToDevice, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_read_counters(raft_sim_t* s, raft_counters_t* out) {
+  if (!s || !out) return fail(-EINVAL, "null argument");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  unsigned long long buf[RAFT_CTR_COUNT + 1];
+  HIP_OK(hipMemcpyAsync(buf, s->d.ctr, sizeof buf, hipMemcpyDeviceToHost, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] = buf[i];
+  out->first_violation_tick = buf[RAFT_CTR_COUNT];
+  out->node_ticks = (uint64_t)s->NN * s->tick;
+  return 0;
+}
+
+int raft_sim_digest(raft_sim_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
+  int rc = check_range(s, c0, nc);
+  if (rc) return rc;
+  if (!out) return fail(-EINVAL, "null output");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  unsigned long long* dout = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&dout), std::max<size_t>(nc, 1) * 8));
+  hipError_t e = rs::launch_digest(s->d, c0, nc, dout, s->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out, dout, (size_t)nc * 8, hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return fail(-EIO, "HIP error in digest: %s", hipGetErrorString(e));
+  return 0;
+}
+

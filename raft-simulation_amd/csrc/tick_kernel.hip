@@ -1,0 +1,646 @@
+// tick_kernel.hip — the batched Raft tick kernel for gfx950 (MI355X) and its helpers.
+//
+// One lane per node, one wave per floor(64/N) clusters, `nt` ticks fused per launch with all hot
+// node state in VGPRs. Per tick a lane does the reference's `wait` (src/raft/core.clj:176-195) once:
+// pick at most one event (D3), run the handler (core.clj:91-169, log.clj:5-87), emit messages into
+// LDS cells, then — only when some lane of the wave did something — the wave runs the network
+// (P2), log transfer (P3) and checker (P4) phases of SIM_SPEC.md §4. Idle ticks cost a handful of
+// VALU instructions and one ballot.
+#include "device.hpp"
+
+namespace rs {
+
+__device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) {
+  atomicAdd(&lctr[kind], 1u);
+  atomicMin(&lctr[LCTR_FIRSTVIOL], t);
+}
+
+__device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t ev, uint32_t src,
+                                                uint32_t mterm, uint32_t role, uint32_t term,
+                                                uint32_t fault) {
+  h = fnv(h, t);
+  h = fnv(h, ev);
+  h = fnv(h, src);
+  h = fnv(h, mterm);
+  h = fnv(h, role);
+  h = fnv(h, term);
+  return fnv(h, fault);
+}
+
+// P2 fault draws for one emitted message, written into the (sender, receiver) LDS cell.
+template <int N>
+__device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
+                                         uint32_t p, bool part, uint32_t sides, uint32_t* cl,
+                                         uint4 a, uint4 b, uint32_t& sentmask, uint32_t* lctr) {
+  lctr_add(lctr, RAFT_CTR_SENT, 1);
+  if (part && (((sides >> id) ^ (sides >> p)) & 1)) {
+    lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
+    return;
+  }
+  uint32_t pack;
+  if (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax) {
+    pack = S.dmin | 1u << 16;
+  } else {
+    const uint4 w = philox(g, id | P_NET << 8, t, p, S.key0, S.key1);
+    if (ppm(w.x) < S.drop_ppm) {
+      lctr_add(lctr, RAFT_CTR_DROPPED, 1);
+      return;
+    }
+    const uint32_t span = S.dmax - S.dmin + 1;
+    pack = (S.dmin + __umulhi(w.z, span)) | 1u << 16;
+    if (ppm(w.y) < S.dup_ppm) {
+      lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
+      pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
+    }
+  }
+  b.w = pack;
+  reinterpret_cast<uint4*>(cl)[0] = a;
+  reinterpret_cast<uint4*>(cl)[1] = b;
+  sentmask |= 1u << p;
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+  constexpr int CPW = 64 / N;
+  constexpr int CELL_WORDS = CPW * N * N * 8;
+  constexpr int WAVE_WORDS = CELL_WORDS + LCTR_WORDS;
+  constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* cells = smem + wv * WAVE_WORDS;
+  uint32_t* lctr = cells + CELL_WORDS;
+  if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+
+  const uint32_t wave = blockIdx.x * 4 + wv;
+  const int cs = lane / N, k = lane - cs * N;
+  const uint32_t c = wave * CPW + cs;
+  const bool active = lane < CPW * N && c < S.C;
+  const uint32_t gi = c * N + k, id = k + 1, peers = ALL & ~(1u << id);
+  const uint32_t g = S.goff + c;
+  const int bl = (cs < CPW ? cs : 0) * N;
+  const uint32_t NN = S.NN, A = S.A;
+  uint32_t* mycells = cells + (cs < CPW ? cs : 0) * N * N * 8;
+
+  NodeR n = {};
+  uint32_t hidx = 0, hterm = 0, hval = 0;
+  if (active) {
+    const uint32_t fl = S.flags[gi], mk = S.masks[gi], qm = S.qmeta[gi];
+    n.role = fl & 3; n.vf = (fl >> 2) & 15; n.lid = (fl >> 6) & 15; n.fault = (fl >> 10) & 7;
+    n.seq = (fl >> 13) & 1; n.lsp = (fl >> 14) & 1;
+    n.votes = mk & 0xFFFF; n.keys = mk >> 16;
+    n.term = S.term[gi]; n.commit = S.commit[gi]; n.len = S.len[gi]; n.deadline = S.deadline[gi];
+    n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
+    n.rq.arr = S.req_arr[gi]; n.rs.arr = S.res_arr[gi];
+    n.rq.tail = S.req_tail[gi]; n.rs.tail = S.res_tail[gi];
+    n.base = S.abase[gi]; n.front = S.afront[gi]; n.led = S.led[gi];
+    n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
+    hidx = S.hwm[c * 4]; hterm = S.hwm[c * 4 + 1]; hval = S.hwm[c * 4 + 2];
+  }
+  uint2* const myar = active ? arena_of(S, gi) : nullptr;
+
+  uint4 cw = make_uint4(0, 0, 0, 0);
+  for (uint32_t t = t0; t != t0 + nt; ++t) {
+    // ---------------------------------------------------------------- P0 client injection (D9)
+    bool inj = false;
+    uint32_t injv = 0;
+    if (S.client_ppm) {
+      if (t == t0 || (t & 3) == 0) cw = philox(g, P_CLIENT << 8, t >> 2, 0, S.key0, S.key1);
+      const uint32_t sel = t & 3;
+      const uint32_t wsel = sel == 0 ? cw.x : sel == 1 ? cw.y : sel == 2 ? cw.z : cw.w;
+      if (active && ppm(wsel) < S.client_ppm) {
+        const uint4 d = philox(g, P_CLIENT_DETAIL << 8, t, 0, S.key0, S.key1);
+        if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
+        if (1 + __umulhi(d.x, N) == id) {
+          inj = true;
+          injv = d.y;
+        }
+      }
+    }
+    const bool live = active && !n.fault;
+    const bool ev0 = live && (n.rq.arr <= t || n.rs.arr <= t || t >= n.deadline);
+    if (__ballot(ev0 || inj) == 0) continue;  // idle tick for every cluster of this wave
+
+    if (inj) qinsert(S, gi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                     make_uint4(0, 0, 0, 0), lctr);
+
+    // ---------------------------------------------------------------- P1 one event per node
+    const bool req_ok = live && n.rq.arr <= t;
+    const bool res_ok = live && n.rs.arr <= t;
+    uint32_t sentmask = 0;
+    uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, pold_len = 0,
+             preloc = 0, pet = 0, pev = 0;
+    int appended_at = -1;
+    bool elected = false, mchg = false;
+    if (live && (req_ok || res_ok || t >= n.deadline)) {
+      const uint4 w = philox(g, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+      int which = -1;
+      if (req_ok && res_ok) which = (w.x & 1) ? 1 : 0;   // alts!! choice, core.clj:181
+      else if (req_ok) which = 0;
+      else if (res_ok) which = 1;
+      uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
+      if (which == 0) qpop(S, gi, 0, n.rq, m0, m1);
+      else if (which == 1) qpop(S, gi, 1, n.rs, m0, m1);
+      const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
+                     mpoff = m1.w;
+      const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
+                     mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
+
+      NodeR nn = n;
+      uint32_t fault = 0, ev = 0;
+      int emit = 0;                 // 1 request-vote bcast, 2 append-entries bcast, 3 one reply
+      int nm = 0;                   // next/match: 1 init, 2 clear, 3 dec next[src], 4 set src
+      uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);  // reply cell words
+      uint32_t appended = 0, applied = 0;
+
+      if (which < 0) {
+        if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
+          ev = 7;
+          emit = 2;
+        } else {                                            // timeout-handler 166-169
+          ev = 6;
+          nn.role = RAFT_CANDIDATE; nn.vf = id; nn.votes = 1u << id; nn.term = n.term + 1;
+          if (n.commit > n.len) {                           // last-entry (log.clj:47-49)
+            fault = RAFT_FAULT_IOOBE;
+          } else {
+            uint32_t ep = 0, et = 0, evl = 0;
+            if (n.commit) {
+              const uint2 e = myar[(n.base + n.commit - 1) % A];
+              ep = 1; et = e.x; evl = e.y;
+            }
+            ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, nn.term, n.commit, 0);
+            rb = make_uint4(et, evl, 0, 0);
+            emit = 1;
+          }
+        }
+      } else {
+        ev = type;
+        switch (type) {
+          case RAFT_MSG_REQUEST_VOTE: {                     // request-vote-handler 91-103
+            uint32_t consistent = 1;
+            if (!(S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) && ma != 0) {
+              if (ma > n.len) {
+                fault = RAFT_FAULT_IOOBE;
+              } else {
+                const uint2 e = myar[(n.base + ma - 1) % A];
+                consistent = mep && e.x == met && e.y == mev;
+              }
+            }
+            if (fault) break;
+            const uint32_t grant = mterm >= n.term && n.vf == 0 && consistent;
+            if (grant) nn.vf = src;
+            ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
+            emit = 3;
+            break;
+          }
+          case RAFT_MSG_APPEND_ENTRIES: {                   // append-entries-handler 105-123
+            uint32_t consistent = 1;
+            if (mb != 0) {
+              if (mb > n.len) {
+                fault = RAFT_FAULT_IOOBE;
+                break;
+              }
+              const uint2 e = myar[(n.base + mb - 1) % A];
+              consistent = mep && e.x == met && e.y == mev;
+            }
+            if (mterm < n.term) {
+              ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
+            } else if (!consistent) {
+              ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
+              nn.len = n.len > mb ? n.len - mb : 0;         // remove-from! 78-81
+              nn.seq = 1;
+            } else {
+              if (n.len + pcnt > S.L) {
+                fault = RAFT_FAULT_OVERFLOW;
+                break;
+              }
+              pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff; ppcnt = pcnt;
+              pold_base = n.base; pold_len = n.len;
+              if (pcnt) {                                    // append-entries! 61-64
+                if (n.base + n.len != n.front) {
+                  preloc = 1;
+                  nn.base = n.front;
+                  nn.front = n.front + n.len;
+                }
+                nn.front += pcnt;
+                appended_at = (int)n.len;
+              }
+              nn.len = n.len + pcnt;
+              nn.seq = 0;
+              appended = pcnt;
+              nn.commit = nn.len;                            // apply-entries! 69-76
+              applied = nn.commit > n.commit ? nn.commit - n.commit : 0;
+              ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
+              nn.role = RAFT_FOLLWER; nn.vf = 0; nn.votes = 0;   // candidate->follower 75-78
+              nn.lid = src; nn.term = mterm;
+            }
+            emit = 3;
+            break;
+          }
+          case RAFT_MSG_CLIENT_SET: {                        // client-set-handler 151-160
+            if (n.role != RAFT_LEADER) break;                // redirect-client only
+            if (n.len + 1 > S.L) {
+              fault = RAFT_FAULT_OVERFLOW;
+              break;
+            }
+            pkind = PLAN_ENTRY; pet = n.term; pev = ma;
+            pold_base = n.base; pold_len = n.len;
+            if (n.base + n.len != n.front) {
+              preloc = 1;
+              nn.base = n.front;
+              nn.front = n.front + n.len;
+            }
+            nn.front += 1;
+            nn.len = n.len + 1;
+            nn.seq = 0;
+            appended = 1;
+            appended_at = (int)n.len;
+            break;
+          }
+          case RAFT_MSG_VOTE_RESPONSE: {                     // vote-response-handler 125-139
+            if (n.commit > n.len) {                          // last-entry first
+              fault = RAFT_FAULT_IOOBE;
+              break;
+            }
+            if (mterm > n.term) {
+              nn.term = mterm;
+              nn.role = RAFT_FOLLWER; nn.vf = 0; nn.votes = 0;
+            } else if (flag && n.role == RAFT_CANDIDATE) {
+              const uint32_t votes = n.votes | 1u << src;
+              if (__popc(votes) < (N + 1) / 2) {             // majority? 19-21
+                nn.votes = votes;
+              } else {                                       // candidate->leader 80-84
+                nn.role = RAFT_LEADER; nn.vf = 0; nn.votes = 0; nn.lid = id;
+                nn.lsp = 1; nn.keys = peers;                 // leader-state 40-42
+                nm = 1;
+                emit = 2;
+                elected = true;
+              }
+            }
+            break;
+          }
+          case RAFT_MSG_APPEND_RESPONSE: {                   // append-response-handler 141-149
+            if (mterm > n.term) {                            // leader->follower 86-89
+              nn.term = mterm;
+              nn.role = RAFT_FOLLOWER; nn.lid = 0; nn.lsp = 0; nn.keys = 0;
+              nm = 2;
+            } else if (!flag) {
+              if (!n.lsp || !((n.keys >> src) & 1)) {
+                fault = RAFT_FAULT_NPE;                      // (dec nil)
+                break;
+              }
+              nm = 3;
+            } else {
+              nn.lsp = 1;
+              nn.keys |= 1u << src;
+              nm = 4;
+              mchg = true;
+            }
+            break;
+          }
+          default:
+            break;
+        }
+      }
+      // append-entries-rpc (core.clj:56-67) preconditions: last-entry, then per peer (- nil 1)
+      // and subvec-of-LazySeq, in doseq order.
+      if (emit == 2 && !fault) {
+        const uint32_t first = id == 1 ? 2u : 1u;
+        if (nn.commit > nn.len) fault = RAFT_FAULT_IOOBE;
+        else if (!nn.lsp || !((nn.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
+        else if (nn.seq) fault = RAFT_FAULT_CCE;
+        else if ((nn.keys & peers) != peers) fault = RAFT_FAULT_NPE;
+      }
+      const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
+      if (fault) {                                   // D8: halt with the pre-event state
+        n.fault = fault;
+        n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
+        lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
+        pkind = PLAN_NONE;
+        appended_at = -1;
+        elected = false;
+        mchg = false;
+      } else {
+        nn.deadline = nn.role == RAFT_LEADER ? t + S.hb
+                                             : t + S.el_base + __umulhi(w.y, S.el_span);
+        nn.trace = trace_event(n.trace, t, ev, tsrc, tterm, nn.role, nn.term, 0);
+        // leader-state words (cold, in HBM)
+        if (nm == 1 || nm == 2) {
+#pragma unroll
+          for (int p = 1; p <= N; ++p) {
+            S.next[(p - 1) * NN + gi] = (nm == 1 && p != (int)id) ? (int32_t)(n.commit + 1) : 0;
+            S.match[(p - 1) * NN + gi] = 0;
+          }
+        } else if (nm == 3) {
+          S.next[(src - 1) * NN + gi] -= 1;
+        } else if (nm == 4) {
+          S.next[(src - 1) * NN + gi] = (int32_t)mb;
+          S.match[(src - 1) * NN + gi] = (int32_t)ma;
+        }
+        n = nn;
+        lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
+        lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
+        lctr_add(lctr, RAFT_CTR_ENTRIES_APPLIED, applied);
+        if (elected) {
+          lctr_add(lctr, RAFT_CTR_LEADERS, 1);
+          n.led = n.term;
+        }
+        // ------------------------------------------------ emission (rpc / respond)
+        if (emit) {
+          bool part = false;
+          uint32_t sides = 0;
+          if (S.part_ppm) {
+            const uint4 pw = philox(g, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
+            part = ppm(pw.x) < S.part_ppm;
+            sides = pw.y;
+          }
+          if (emit == 3) {
+            transmit<N>(S, g, t, id, src, part, sides, mycells + ((k * N) + src - 1) * 8, ra, rb,
+                        sentmask, lctr);
+          } else {
+#pragma unroll
+            for (int p = 1; p <= N; ++p) {
+              if (p == (int)id) continue;
+              if (emit == 2) {
+                const int32_t nx = S.next[(p - 1) * NN + gi];
+                const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
+                const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
+                uint32_t ep = 0, et = 0, evl = 0, pc = 0, po = 0;
+                if (start < n.len) {
+                  const uint2 e = myar[(n.base + start) % A];
+                  ep = 1; et = e.x; evl = e.y;
+                  pc = n.len - start - 1;
+                  po = pc ? n.base + start + 1 : 0;
+                }
+                ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
+                                n.commit, (uint32_t)prev);
+                rb = make_uint4(et, evl, po, 0);
+              }
+              transmit<N>(S, g, t, id, p, part, sides, mycells + ((k * N) + p - 1) * 8, ra, rb,
+                          sentmask, lctr);
+            }
+          }
+        }
+      }
+    }
+
+    // ---------------------------------------------------------------- P2 network delivery
+    if (__ballot(sentmask != 0)) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+      for (int s = 0; s < N; ++s) {
+        const uint32_t sm = __shfl(sentmask, bl + s);
+        if (active && s != k && ((sm >> id) & 1)) {
+          const uint4* cl = reinterpret_cast<const uint4*>(mycells + (s * N + k) * 8);
+          const uint4 a = cl[0], b = cl[1];
+          const uint32_t copies = b.w >> 16;
+          const uint4 mb0 = make_uint4(t + (b.w & 0xFF), a.x, a.y, a.z);
+          const uint4 mb1 = make_uint4(a.w, b.x, b.y, b.z);
+          const uint4 mc0 = make_uint4(t + ((b.w >> 8) & 0xFF), a.x, a.y, a.z);
+          if ((a.x & 7) <= RAFT_MSG_CLIENT_SET) {
+            qinsert(S, gi, n.fault, 0, n.rq, mb0, mb1, lctr);
+            if (copies == 2) qinsert(S, gi, n.fault, 0, n.rq, mc0, mb1, lctr);
+          } else {
+            qinsert(S, gi, n.fault, 1, n.rs, mb0, mb1, lctr);
+            if (copies == 2) qinsert(S, gi, n.fault, 1, n.rs, mc0, mb1, lctr);
+          }
+        }
+      }
+    }
+
+    // ---------------------------------------------------------------- P3 log writes
+    if (__ballot(pkind != PLAN_NONE)) {
+      const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
+      const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
+      if (pkind != PLAN_NONE && m) {
+        if (preloc)
+          for (uint32_t i = 0; i < pold_len; ++i)
+            myar[(n.base + i) % A] = myar[(pold_base + i) % A];
+        const uint32_t dst = n.base + pold_len;
+        if (pkind == PLAN_ENTRY) {
+          myar[dst % A] = make_uint2(pet, pev);
+        } else {
+          const uint2* sa = arena_of(S, c * N + psrc - 1);
+          uint32_t evicted = 0;
+          for (uint32_t i = 0; i < m; ++i) {
+            uint2 e = make_uint2(0, 0);
+            if ((uint64_t)sfront > (uint64_t)ppoff + i + A) ++evicted;
+            else e = sa[(ppoff + i) % A];
+            myar[(dst + i) % A] = e;
+          }
+          lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
+        }
+      }
+    }
+
+    // ---------------------------------------------------------------- P4 invariant checker
+    if (__ballot(elected || appended_at >= 0 || mchg)) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      if (__ballot(elected)) {                       // election safety
+        bool bad = false;
+#pragma unroll
+        for (int s = 0; s < N; ++s) {
+          const uint32_t ls = __shfl(n.led, bl + s);
+          bad |= elected && s != k && ls == n.led;
+        }
+        if (bad) violation(lctr, RAFT_CTR_VIOL_ELECTION, t);
+      }
+      if (__ballot(appended_at >= 0)) {              // log matching
+        bool bad = false;
+#pragma unroll
+        for (int s = 0; s < N; ++s) {
+          const uint32_t sb = __shfl(n.base, bl + s), sl = __shfl(n.len, bl + s);
+          if (appended_at >= 0 && s != k && !bad) {
+            const uint2* oa = arena_of(S, c * N + s);
+            const uint32_t hi = n.len < sl ? n.len : sl;
+            for (uint32_t p = (uint32_t)appended_at; p < hi; ++p) {
+              const uint2 x = myar[(n.base + p) % A], y = oa[(sb + p) % A];
+              if (x.x == y.x && x.y != y.y) {
+                bad = true;
+                break;
+              }
+            }
+          }
+        }
+        if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
+      }
+      if (elected && hidx > 0) {                     // leader completeness (pre-tick hwm)
+        bool ok = n.len >= hidx;
+        if (ok) {
+          const uint2 e = myar[(n.base + hidx - 1) % A];
+          ok = e.x == hterm && e.y == hval;
+        }
+        if (!ok) violation(lctr, RAFT_CTR_VIOL_COMPLETE, t);
+      }
+      int32_t cm = -1;
+      uint32_t ct = 0, cv = 0;
+      if (active && n.role == RAFT_LEADER && (elected || mchg)) {
+        int32_t vals[N];
+        vals[0] = (int32_t)n.len;
+        int j = 1;
+#pragma unroll
+        for (int p = 1; p <= N; ++p) {
+          if (p == (int)id) continue;
+          vals[j++] = ((n.keys >> p) & 1) ? S.match[(p - 1) * NN + gi] : 0;
+        }
+#pragma unroll
+        for (int i = 1; i < N; ++i)
+#pragma unroll
+          for (int q = i; q > 0; --q)
+            if (vals[q - 1] < vals[q]) {
+              const int32_t tmp = vals[q]; vals[q] = vals[q - 1]; vals[q - 1] = tmp;
+            }
+        int32_t mm = vals[(N + 1) / 2 - 1];
+        if (mm > (int32_t)n.len) mm = (int32_t)n.len;
+        if (mm > (int32_t)hidx) {
+          cm = mm;
+          const uint2 e = myar[(n.base + (uint32_t)mm - 1) % A];
+          ct = e.x; cv = e.y;
+        }
+      }
+      if (__ballot(cm >= 0)) {                       // cluster argmax, lowest id on ties
+        int32_t best = -1;
+        uint32_t bt = 0, bv = 0;
+#pragma unroll
+        for (int s = 0; s < N; ++s) {
+          const int32_t sm = __shfl(cm, bl + s);
+          const uint32_t st = __shfl(ct, bl + s), sv = __shfl(cv, bl + s);
+          if (sm > best) { best = sm; bt = st; bv = sv; }
+        }
+        if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- write back
+  if (active) {
+    S.flags[gi] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
+    S.masks[gi] = n.votes | n.keys << 16;
+    S.term[gi] = n.term; S.commit[gi] = n.commit; S.len[gi] = n.len; S.deadline[gi] = n.deadline;
+    S.qmeta[gi] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
+    S.req_arr[gi] = n.rq.arr; S.res_arr[gi] = n.rs.arr;
+    S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
+    S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
+    S.trace_lo[gi] = (uint32_t)n.trace; S.trace_hi[gi] = (uint32_t)(n.trace >> 32);
+    if (k == 0) {
+      S.hwm[c * 4] = hidx; S.hwm[c * 4 + 1] = hterm; S.hwm[c * 4 + 2] = hval;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (lane < RAFT_CTR_COUNT) {
+    const uint32_t v = lctr[lane];
+    if (v) atomicAdd(&S.ctr[lane], (unsigned long long)v);
+  } else if (lane == LCTR_FIRSTVIOL) {
+    const uint32_t v = lctr[lane];
+    if (v != INF) atomicMin(&S.ctr[RAFT_CTR_COUNT], (unsigned long long)v);
+  }
+}
+
+// Initial state: init-node (core.clj:31-38) and an empty log (log.clj:33-34) for every node.
+__global__ void init_kernel(DevSim S) {
+  const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= S.NN) return;
+  const uint32_t c = gi / S.N, id = gi - c * S.N + 1;
+  const uint4 w = philox(S.goff + c, id | P_INIT << 8, 0, 0, S.key0, S.key1);
+  S.flags[gi] = 0; S.masks[gi] = 0; S.term[gi] = 1; S.commit[gi] = 0; S.len[gi] = 0;
+  S.deadline[gi] = S.el_base + __umulhi(w.y, S.el_span);
+  S.qmeta[gi] = 0; S.req_arr[gi] = INF; S.res_arr[gi] = INF; S.req_tail[gi] = 0;
+  S.res_tail[gi] = 0; S.abase[gi] = 0; S.afront[gi] = 0; S.led[gi] = 0;
+  S.trace_lo[gi] = 0x84222325u; S.trace_hi[gi] = 0xCBF29CE4u;
+}
+
+// Per-cluster canonical digest (SIM_SPEC §6), one thread per cluster.
+__global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long long* out) {
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nc) return;
+  const uint32_t c = c0 + ci, N = S.N, NN = S.NN;
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (uint32_t k = 0; k < N; ++k) {
+    const uint32_t gi = c * N + k;
+    const uint32_t fl = S.flags[gi], mk = S.masks[gi], qm = S.qmeta[gi];
+    const uint32_t w[12] = {fl & 3, (fl >> 2) & 15, (fl >> 6) & 15, (fl >> 10) & 7,
+                            (fl >> 13) & 1, (fl >> 14) & 1, mk & 0xFFFF, mk >> 16, S.term[gi],
+                            S.commit[gi], S.len[gi], S.deadline[gi]};
+    for (int i = 0; i < 12; ++i) h = fnv(h, w[i]);
+    for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)S.next[p * NN + gi]);
+    for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)S.match[p * NN + gi]);
+    h = fnv(h, S.led[gi]);
+    h = fnv(h, S.trace_lo[gi]);
+    h = fnv(h, S.trace_hi[gi]);
+    h = fnv(h, S.abase[gi]);
+    h = fnv(h, S.afront[gi]);
+    const uint32_t qh[2] = {qm & 15, (qm >> 9) & 15}, qc[2] = {(qm >> 4) & 31, (qm >> 13) & 31};
+    for (int which = 0; which < 2; ++which) {
+      h = fnv(h, qc[which]);
+      const uint32_t* qb = qslots(S, gi, which);
+      for (uint32_t i = 0; i < qc[which]; ++i) {
+        const uint32_t* m = qb + ((qh[which] + i) % S.Q) * 8;
+        for (int j = 0; j < 8; ++j) h = fnv(h, m[j]);
+      }
+    }
+    const uint2* ar = arena_of(S, gi);
+    const uint32_t base = S.abase[gi], len = S.len[gi];
+    for (uint32_t i = 0; i < len; ++i) {
+      const uint2 e = ar[(base + i) % S.A];
+      h = fnv(h, e.x);
+      h = fnv(h, e.y);
+    }
+  }
+  h = fnv(h, S.hwm[c * 4]);
+  h = fnv(h, S.hwm[c * 4 + 1]);
+  h = fnv(h, S.hwm[c * 4 + 2]);
+  out[ci] = h;
+}
+
+template <int N>
+hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+  constexpr int CPW = 64 / N;
+  constexpr size_t lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
+  const uint32_t waves = (S.C + CPW - 1) / CPW;
+  const uint32_t blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL(tick_kernel<N>, dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  return hipGetLastError();
+}
+
+hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+  switch (S.N) {
+    case 2: return launch_tick_n<2>(S, t0, nt, st);
+    case 3: return launch_tick_n<3>(S, t0, nt, st);
+    case 4: return launch_tick_n<4>(S, t0, nt, st);
+    case 5: return launch_tick_n<5>(S, t0, nt, st);
+    case 6: return launch_tick_n<6>(S, t0, nt, st);
+    case 7: return launch_tick_n<7>(S, t0, nt, st);
+    case 8: return launch_tick_n<8>(S, t0, nt, st);
+    case 9: return launch_tick_n<9>(S, t0, nt, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int N>
+hipError_t configure_n() {
+  constexpr int CPW = 64 / N;
+  constexpr int lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+hipError_t configure_kernels() {
+  hipError_t e = hipSuccess;
+  if ((e = configure_n<2>()) || (e = configure_n<3>()) || (e = configure_n<4>()) ||
+      (e = configure_n<5>()) || (e = configure_n<6>()) || (e = configure_n<7>()) ||
+      (e = configure_n<8>()) || (e = configure_n<9>()))
+    return e;
+  return hipSuccess;
+}
+
+hipError_t launch_init(const DevSim& S, hipStream_t st) {
+  hipLaunchKernelGGL(init_kernel, dim3((S.NN + 255) / 256), dim3(256), 0, st, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(digest_kernel, dim3((nc + 127) / 128), dim3(128), 0, st, S, c0, nc, out);
+  return hipGetLastError();
+}
+
+}  // namespace rs

@@ -1,6 +1,7 @@
 """Shared test helpers: oracle handles and state comparison (test infrastructure)."""
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -49,3 +50,53 @@ def compare_py_backend(pc: "pyref.PyCluster", be: Backend, cluster: int):
                     A = len(ar)
                     assert [ar[(g[7] + k) % A] for k in range(pcnt)] == [tuple(e) for e in w[7]]
     assert be.read_hwm(cluster, 1)[0] == tuple(pc.hwm)
+
+
+def gpu(**cfg):
+    import raftsim
+    return raftsim.Simulator(**cfg)
+
+
+def oracle_threads(be, n):
+    be._lib.raft_ref_set_threads(be._h, n)
+
+
+def cpu_threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def describe_cluster_diff(a, b, cluster):
+    """Human-readable differences between cluster `cluster` of two backends."""
+    lines = []
+    ra, rb = a.read_nodes(cluster, 1), b.read_nodes(cluster, 1)
+    for i, (x, y) in enumerate(zip(ra, rb)):
+        for f in x:
+            if x[f] != y[f]:
+                lines.append(f"  node {i + 1} {f}: {x[f]} != {y[f]}")
+        for which in (0, 1):
+            qa, qb = a.read_queue(cluster, i + 1, which), b.read_queue(cluster, i + 1, which)
+            if qa != qb:
+                lines.append(f"  node {i + 1} queue {which}: {qa} != {qb}")
+        la, lb = a.log(cluster, i + 1), b.log(cluster, i + 1)
+        if la != lb:
+            lines.append(f"  node {i + 1} log: {la[:12]}... != {lb[:12]}...")
+    ha, hb = a.read_hwm(cluster, 1), b.read_hwm(cluster, 1)
+    if ha != hb:
+        lines.append(f"  hwm {ha} != {hb}")
+    return "\n".join(lines)
+
+
+def bisect_divergence(cfg, g, max_ticks, make_a, make_b):
+    """Re-run global cluster g alone, one tick at a time, and report the first divergent tick."""
+    one = dict(cfg, n_clusters=1, cluster_offset=g)
+    a, b = make_a(**one), make_b(**one)
+    prev = None
+    for t in range(max_ticks):
+        a.step(1)
+        b.step(1)
+        if a.digest()[0] != b.digest()[0]:
+            return (f"cluster {g} first diverges at tick {t}:\n"
+                    + describe_cluster_diff(a, b, 0)
+                    + (f"\n  state before tick {t} (a):\n{prev}" if prev else ""))
+        prev = "\n".join(f"    {r}" for r in a.read_nodes(0, 1)) if t % 1 == 0 else prev
+    return f"cluster {g}: no divergence in {max_ticks} single-tick steps (launch-size effect?)"
