@@ -83,12 +83,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if "RANK" in os.environ and "MASTER_ADDR" in os.environ:     # launched by torchrun
         import torch
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl")                           # RCCL on ROCm
 
     import raftsim
 
@@ -120,18 +120,14 @@ def main():
     delta = {k: (c_after[k] - c_before[k]) for k in c_after if k != "first_violation_tick"}
 
     elapsed_max = elapsed
-    total_node_ticks = delta["node_ticks"]
     if dist is not None:
-        import torch
+        from raftsim import dist as rdist
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed_max = float(t.item())
-        names = sorted(delta)
-        v = torch.tensor([delta[k] for k in names], dtype=torch.int64, device=f"cuda:{local_rank}")
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        delta = dict(zip(names, (int(x) for x in v.tolist())))
-        total_node_ticks = delta["node_ticks"]
+        dev = f"cuda:{local_rank}"
+        elapsed_max = rdist.reduce_max(elapsed, dev)
+        delta = rdist.reduce_counters(dict(delta, first_violation_tick=None), dev)
+        kernel_ms = rdist.reduce_max(kernel_ms, dev)
+    total_node_ticks = delta["node_ticks"]
 
     if rank == 0:
         bpnt, m, e = algorithmic_bytes_per_node_tick(NODES, delta)
@@ -164,7 +160,7 @@ def main():
                          "algorithmic_bytes_per_node_tick": bpnt,
                          "msgs_per_node_tick": m, "entries_per_node_tick": e,
                          "avg_launch_ms": avg_launch_ms, "ticks_per_launch": ticks_per_launch},
-            "counters": {k: v for k, v in delta.items() if v},
+            "counters": {k: v for k, v in delta.items() if v and k != "first_violation_tick"},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(42)

@@ -1,0 +1,44 @@
+"""Multi-GPU plumbing: cluster-range sharding and the counter all-reduce.
+
+Clusters are independent and Philox streams are keyed by the global cluster id (SIM_SPEC D13),
+so a rank simulates a contiguous range of clusters with no data-path exchange. The only
+collective is the end-of-run reduction of the counter vector (SUM) and the first-violation tick
+(MIN): a few hundred bytes, latency-bound, over RCCL (torch.distributed backend "nccl") on the GPU
+box or gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+NONE_TICK = 2 ** 63 - 1
+
+
+def shard(total_clusters: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [offset, offset + count) range of global cluster ids owned by `rank`."""
+    lo = total_clusters * rank // world
+    hi = total_clusters * (rank + 1) // world
+    return lo, hi - lo
+
+
+def reduce_counters(c: dict, device=None) -> dict:
+    """All-reduce a counters dict (raftsim Backend.counters()) over the default process group."""
+    import torch
+    import torch.distributed as dist
+
+    names = sorted(k for k in c if k != "first_violation_tick")
+    v = torch.tensor([int(c[k]) for k in names], dtype=torch.int64, device=device)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    fv = c.get("first_violation_tick")
+    f = torch.tensor([NONE_TICK if fv is None else int(fv)], dtype=torch.int64, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    out = dict(zip(names, (int(x) for x in v.tolist())))
+    fmin = int(f.item())
+    out["first_violation_tick"] = None if fmin == NONE_TICK else fmin
+    return out
+
+
+def reduce_max(x: float, device=None) -> float:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,71 @@
+"""Regenerate the golden fixtures from the Python restatement (oracle/pyref.py).
+
+The reference itself cannot run here (Clojure 1.6 on a JVM; no JVM in this image), so the fixtures
+are the Python restatement's outputs: per-event traces and final canonical states for small seeded
+runs. tests/test_golden.py checks the C oracle (CPU) and libraftsim.so (GPU) against them.
+Run: python tests/golden/make_golden.py
+"""
+import json
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent / "oracle"))
+import pyref  # noqa: E402
+
+CASES = {
+    # BASELINE config 1: single 5-node cluster, seed 42, 10k ticks, no faults (full event trace)
+    "c1_seed42": dict(cfg=dict(nodes=5, seed=42), gid=0, ticks=10000, trace=True),
+    "c1_seed1": dict(cfg=dict(nodes=5, seed=1), gid=0, ticks=10000, trace=True),
+    "faults_n5": dict(cfg=dict(nodes=5, seed=7, drop_ppm=100000, dup_ppm=20000, dmin=1, dmax=30,
+                               part_ppm=100000, client_ppm=1500, log_cap=128), gid=3,
+                      ticks=30000, trace=True),
+    "client_n7": dict(cfg=dict(nodes=7, seed=11, client_ppm=3000, log_cap=256), gid=5,
+                      ticks=20000, trace=False),
+    "overflow_n9": dict(cfg=dict(nodes=9, seed=13, inbox_cap=2, dup_ppm=300000, dmax=3,
+                                 client_ppm=5000, log_cap=64), gid=1, ticks=20000, trace=False),
+    "variant_n3": dict(cfg=dict(nodes=3, seed=17, variant_flags=1, client_ppm=150,
+                                drop_ppm=50000, log_cap=64), gid=2, ticks=30000, trace=False),
+}
+
+
+class Tracer(pyref.PyCluster):
+    """PyCluster that records (tick, node, trace-hash) whenever a node's trace hash changes."""
+
+    def step(self, t):
+        before = dict(self.trace)
+        super().step(t)
+        for i in sorted(self.trace):
+            if self.trace[i] != before[i]:
+                n = self.canonical_node(i)
+                self.events.append([t, i, n["role"], n["current_term"], n["fault"],
+                                    format(self.trace[i], "016x")])
+
+
+def make(name, spec):
+    cfg = pyref.default_config(**spec["cfg"])
+    c = Tracer(cfg, spec["gid"])
+    c.events = []
+    for t in range(spec["ticks"]):
+        c.step(t)
+    nodes = []
+    for i in range(1, c.N + 1):
+        n = c.canonical_node(i)
+        n["trace_hash"] = format(n["trace_hash"], "016x")
+        n["log"] = [list(e) for e in c.logs[i].entries]
+        n["req"] = [list(m[:7]) + [[list(e) for e in m[7]]] for m in c.canonical_msgs(i, 0)]
+        n["res"] = [list(m[:7]) + [[list(e) for e in m[7]]] for m in c.canonical_msgs(i, 1)]
+        nodes.append(n)
+    out = {"config": spec["cfg"], "cluster_offset": spec["gid"], "ticks": spec["ticks"],
+           "nodes": nodes, "hwm": list(c.hwm), "counters": c.cnt,
+           "first_violation_tick": c.first_violation}
+    if spec["trace"]:
+        out["events"] = c.events
+    (HERE / f"{name}.json").write_text(json.dumps(out, separators=(",", ":")) + "\n")
+    return out
+
+
+if __name__ == "__main__":
+    for name, spec in CASES.items():
+        o = make(name, spec)
+        print(name, {k: v for k, v in o["counters"].items() if v})

@@ -1,0 +1,373 @@
+"""Known-answer scenarios derived by hand from the reference source.
+
+Each scenario builds one cluster's exact state (node maps, logs, queued messages, timers), runs a
+few ticks and checks the outcome the reference's code implies; every expectation cites the lines
+it follows. A scenario can be loaded into the Python restatement (oracle/pyref.py) or into any
+library implementing include/raftsim.h (the C oracle, or libraftsim.so on the GPU), so the same
+hand-derived answers pin all three implementations.
+"""
+from __future__ import annotations
+
+import pyref
+
+BIG = 10 ** 8     # a deadline that never fires inside a scenario
+ROLE = {"follower": 0, "candidate": 1, "leader": 2, "follwer": 3}
+
+
+def node(role="follower", term=1, voted_for=0, leader_id=0, votes=(), ls=None, log=(),
+         commit=0, is_seq=0, deadline=BIG, fault=0, last_led=0):
+    """ls: None (nil leader-state) or {peer: (next, match)}."""
+    return dict(role=ROLE[role], term=term, voted_for=voted_for, leader_id=leader_id,
+                votes=tuple(votes), ls=ls, log=list(log), commit=commit, is_seq=is_seq,
+                deadline=deadline, fault=fault, last_led=last_led)
+
+
+def msg(type, arrival, **f):
+    return dict(type=type, arrival=arrival, **f)
+
+
+class Scenario:
+    def __init__(self, N, nodes, queues=None, hwm=(0, 0, 0), **cfg):
+        self.N, self.nodes, self.hwm = N, nodes, hwm
+        self.queues = queues or {}
+        self.cfg = dict(nodes=N, n_clusters=1, log_cap=64, **cfg)
+
+    # ---------------------------------------------------------------- C ABI backends
+    def load_backend(self, make):
+        be = make(**self.cfg)
+        recs = be.read_nodes_raw(0, 1)
+        for i in range(1, self.N + 1):
+            d, r = self.nodes[i], recs[i - 1]
+            r.role, r.current_term = d["role"], d["term"]
+            r.voted_for, r.leader_id = d["voted_for"], d["leader_id"]
+            r.votes = sum(1 << v for v in d["votes"])
+            r.fault, r.entries_is_seq = d["fault"], d["is_seq"]
+            r.commit_index, r.log_len, r.deadline = d["commit"], len(d["log"]), d["deadline"]
+            r.arena_base, r.arena_frontier = 0, len(d["log"])
+            r.last_led_term = d["last_led"]
+            r.ls_present, r.ls_keys = int(d["ls"] is not None), 0
+            for p in range(self.N):
+                r.next_index[p] = r.match_index[p] = 0
+            for p, (nx, mt) in (d["ls"] or {}).items():
+                r.ls_keys |= 1 << p
+                r.next_index[p - 1], r.match_index[p - 1] = nx, mt
+        be.write_nodes(0, list(recs))
+        for i in range(1, self.N + 1):
+            be.write_arena(0, i, self.nodes[i]["log"])
+        for (i, which), msgs in self.queues.items():
+            be.write_queue(0, i, which, [self._encode(m) for m in msgs])
+        be.write_hwm(0, [self.hwm])
+        return be
+
+    def _encode(self, m):
+        pm = self._py_msg(m)
+        arrival, hdr, term, a, b, et, ev, payload = pyref.encode_msg(m["arrival"], pm)
+        poff = 0
+        if payload:
+            slog = self.nodes[pyref.msg_src(pm)]["log"]
+            assert [tuple(e) for e in slog[len(slog) - len(payload):]] == payload, \
+                "injected payloads must be a suffix of the sender's log"
+            poff = len(slog) - len(payload)
+        return (arrival, hdr, term, a, b, et, ev, poff)
+
+    # ---------------------------------------------------------------- Python restatement
+    @staticmethod
+    def _py_msg(m):
+        pm = {k.replace("_", "-"): v for k, v in m.items() if k != "arrival"}
+        for key in ("last-log-term", "prev-log-term"):
+            if key in pm and pm[key] is not None:
+                pm[key] = tuple(pm[key])
+        if "entries" in pm:
+            pm["entries"] = [tuple(e) for e in pm["entries"]]
+        return pm
+
+    def load_py(self):
+        cfg = pyref.default_config(**{k: v for k, v in self.cfg.items()
+                                      if k in pyref.default_config()})
+        pc = pyref.PyCluster(cfg, 0)
+        names = {v: k for k, v in pyref.ROLE_CODE.items()}
+        for i in range(1, self.N + 1):
+            d = self.nodes[i]
+            ls = None
+            if d["ls"] is not None:
+                ls = {"next-index": {p: nx for p, (nx, _) in d["ls"].items()},
+                      "match-index": {p: mt for p, (_, mt) in d["ls"].items()}}
+            pc.nodes[i] = {"id": i, "state": names[d["role"]], "current-term": d["term"],
+                           "voted-for": d["voted_for"] or None,
+                           "leader-id": d["leader_id"] or None, "leader-state": ls,
+                           "votes": set(d["votes"])}
+            lg = pc.logs[i]
+            lg.entries, lg.is_seq, lg.commit_index = [tuple(e) for e in d["log"]], \
+                bool(d["is_seq"]), d["commit"]
+            pc.deadline[i], pc.fault[i], pc.last_led[i] = d["deadline"], d["fault"], d["last_led"]
+        for (i, which), msgs in self.queues.items():
+            q = pc.req[i] if which == 0 else pc.res[i]
+            q[:] = [(m["arrival"], self._py_msg(m)) for m in msgs]
+        pc.hwm = tuple(self.hwm)
+        return pc
+
+
+class PyView:
+    """Uniform read access to a PyCluster, shaped like the Backend records."""
+
+    def __init__(self, pc):
+        self.pc = pc
+        self.t = 0
+
+    def step(self, n):
+        for _ in range(n):
+            self.pc.step(self.t)
+            self.t += 1
+
+    def node(self, i):
+        return self.pc.canonical_node(i)
+
+    def log(self, i):
+        return [tuple(e) for e in self.pc.logs[i].entries]
+
+    def counters(self):
+        return dict(self.pc.cnt)
+
+
+class BackendView:
+    def __init__(self, be):
+        self.be = be
+
+    def step(self, n):
+        self.be.step(n)
+
+    def node(self, i):
+        return self.be.read_nodes(0, 1)[i - 1]
+
+    def log(self, i):
+        return self.be.log(0, i)
+
+    def counters(self):
+        return self.be.counters()
+
+
+def run(scn, which, make=None):
+    return PyView(scn.load_py()) if which == "py" else BackendView(scn.load_backend(make))
+
+
+# ================================================================ the scenarios
+E1, E2, E3 = (2, 10), (2, 20), (2, 30)
+
+
+def kat_majority(view_of):
+    """majority? (core.clj:19-21): |votes| >= ceil(N/2); N=4 needs only 2 (non-strict)."""
+    assert [pyref.majority(range(n - 1), set(range(k))) for n, k in
+            ((5, 3), (5, 2), (7, 4), (7, 3), (9, 5), (9, 4), (4, 2), (4, 1))] == \
+        [True, False, True, False, True, False, True, False]
+    for n, need in ((4, 2), (5, 3), (7, 4), (9, 5)):
+        # candidate 1 holding need-2 grants besides itself; one more grant -> leader (core.clj:133-138)
+        votes = [1] + list(range(2, need))
+        nodes = {i: node() for i in range(1, n + 1)}
+        nodes[1] = node("candidate", term=2, voted_for=1, votes=votes)
+        q = {(1, 1): [msg("vote-response", 0, term=1, id=need, vote_granted=True)]}
+        v = view_of(Scenario(n, nodes, q))
+        v.step(1)
+        r = v.node(1)
+        assert r["role"] == ROLE["leader"] and r["votes"] == 0 and r["leader_id"] == 1, (n, r)
+        # leader-state (core.clj:40-42): next = commit + 1 = 1, match 0 for every peer
+        assert r["next_index"] == [0] + [1] * (n - 1) and r["match_index"] == [0] * n
+        # one fewer grant stays candidate with the vote recorded (core.clj:134)
+        nodes[1] = node("candidate", term=2, voted_for=1, votes=votes[:-1])
+        v = view_of(Scenario(n, nodes, q))
+        v.step(1)
+        r = v.node(1)
+        if need > 2:
+            assert r["role"] == ROLE["candidate"] and r["votes"] == sum(1 << x for x in votes[:-1] + [need])
+
+
+def kat_first_election(view_of):
+    """Ideal network, 5 nodes from init-node (core.clj:31-38); node 3 times out first."""
+    nodes = {i: node(deadline=BIG) for i in range(1, 6)}
+    nodes[3] = node(deadline=0)
+    v = view_of(Scenario(5, nodes))
+    v.step(1)                                    # t0: timeout-handler (core.clj:166-169)
+    a = v.node(3)
+    assert (a["role"], a["current_term"], a["voted_for"], a["votes"]) == \
+        (ROLE["candidate"], 2, 3, 1 << 3)        # follower->candidate (core.clj:69-73)
+    v.step(1)                                    # t1: every voter runs request-vote-handler
+    for i in (1, 2, 4, 5):
+        r = v.node(i)
+        # grant sets :voted-for but keeps the term (core.clj:97-103 never touches the term)
+        assert (r["role"], r["current_term"], r["voted_for"]) == (ROLE["follower"], 1, 3), r
+    v.step(1)                                    # t2: first grant (from id 1: sender order)
+    assert v.node(3)["votes"] == (1 << 3) | (1 << 1)
+    v.step(1)                                    # t3: second grant -> majority -> leader
+    a = v.node(3)
+    assert (a["role"], a["votes"], a["voted_for"], a["leader_id"]) == (ROLE["leader"], 0, 0, 3)
+    assert a["next_index"] == [1, 1, 0, 1, 1] and a["match_index"] == [0] * 5
+    v.step(1)                                    # t4: followers take the AppendEntries
+    for i in (1, 2, 4, 5):
+        r = v.node(i)
+        # candidate->follower (:follwer, core.clj:76), term and leader from the message (122-123)
+        assert (r["role"], r["current_term"], r["voted_for"], r["leader_id"]) == \
+            (ROLE["follwer"], 2, 0, 3), r
+    v.step(5)                                    # t5: 4th vote (no-op), t6..t9: four replies
+    a = v.node(3)
+    # next-index := log-index = prev 0 + 0 entries; match-index := commit 0 (core.clj:147-149)
+    assert a["next_index"] == [0, 0, 0, 0, 0] and a["role"] == ROLE["leader"]
+    c = v.counters()
+    assert c["leaders"] == 1 and c["ev_vr"] == 4 and c["ev_ar"] == 4 and c["ev_ae"] == 4
+
+
+def kat_duplication(view_of):
+    """AppendEntries appends without truncation (log.clj:61-64) and ships prev+1 (core.clj:61,66)."""
+    ls = {2: (1, 0), 3: (1, 0)}
+    nodes = {1: node("leader", term=2, leader_id=1, ls=ls, log=[E1, E2, E3], deadline=0,
+                     last_led=2),
+             2: node("follwer", term=2, leader_id=1),
+             3: node("follwer", term=2, leader_id=1)}
+    v = view_of(Scenario(3, nodes))
+    v.step(3)        # t0 heartbeat, t1 followers append, t2 leader takes reply from 2
+    assert v.log(2) == [E2, E3] and v.node(2)["commit_index"] == 2    # e1 lost
+    v.step(1)        # t3 reply from 3
+    assert v.node(1)["next_index"][1:] == [2, 2]
+    # second heartbeat 3000 ticks after the leader's last event (hb, core.clj:173): tick 3003,
+    # delivered at 3004
+    v.step(3001)
+    assert v.log(2) == [E2, E3, E3] and v.log(3) == [E2, E3, E3]
+    v.step(3003)
+    assert v.log(2) == [E2, E3, E3, E3]         # one more e3 per heartbeat
+    assert v.counters()["viol_log"] >= 1        # same index and term, different value
+
+
+def kat_truncate_crash(view_of):
+    """Inconsistent AE: drop-last prev (log.clj:78-81), LazySeq; next timeout IOOBE (log.clj:47-49)."""
+    X, Y, Z = (1, 7), (1, 8), (1, 9)
+    # the sender has since crashed (halted), so no later heartbeat re-arms node 2's timer
+    nodes = {1: node("leader", term=2, leader_id=1, ls={2: (3, 0)}, fault=1),
+             2: node("follwer", term=2, leader_id=1, log=[X, Y, Z], commit=3)}
+    q = {(2, 0): [msg("append-entries", 0, term=2, leader_id=1, leader_commit=0,
+                      prev_log_index=2, prev_log_term=(5, 5), entries=[])]}
+    nodes[2]["deadline"] = 1
+    v = view_of(Scenario(2, nodes, q))
+    v.step(1)
+    r = v.node(2)
+    assert r["log_len"] == 1 and r["entries_is_seq"] == 1 and r["commit_index"] == 3
+    assert r["fault"] == 0
+    d = r["deadline"]
+    v.step(d)          # the timeout fires: last-entry (nth (x) 2) throws
+    r = v.node(2)
+    assert r["fault"] == 1 and r["role"] == ROLE["follwer"] and r["current_term"] == 2
+    assert v.counters()["halt_ioobe"] == 1
+
+
+def kat_cce(view_of):
+    """A LazySeq log reaching leadership: entries-from's subvec throws CCE (log.clj:53)."""
+    nodes = {1: node("candidate", term=3, voted_for=1, votes=[1], log=[E1], commit=1, is_seq=1),
+             2: node(), 3: node()}
+    q = {(1, 1): [msg("vote-response", 0, term=1, id=2, vote_granted=True)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(1)
+    r = v.node(1)
+    # halted with the pre-event state: still a candidate with the old votes
+    assert r["fault"] == 3 and r["role"] == ROLE["candidate"] and r["votes"] == 1 << 1
+    assert v.counters()["halt_cce"] == 1 and v.counters()["sent"] == 0
+
+
+def kat_npe(view_of):
+    """append-response failure with nil leader-state: (dec nil) throws NPE (core.clj:146)."""
+    nodes = {1: node("follower", term=2), 2: node()}
+    q = {(1, 1): [msg("append-response", 0, term=2, id=2, success=False)]}
+    v = view_of(Scenario(2, nodes, q))
+    v.step(1)
+    assert v.node(1)["fault"] == 2 and v.counters()["halt_npe"] == 1
+
+
+def kat_partial_leader_state(view_of):
+    """append-response success on a non-leader creates a partial leader-state (core.clj:147-149)."""
+    nodes = {1: node("follower", term=2), 2: node(), 3: node()}
+    q = {(1, 1): [msg("append-response", 0, term=2, id=3, success=True, commit=4, log_index=6)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(1)
+    r = v.node(1)
+    assert r["ls_present"] == 1 and r["ls_keys"] == 1 << 3 and r["role"] == ROLE["follower"]
+    assert r["next_index"][2] == 6 and r["match_index"][2] == 4
+
+
+def kat_stale_step_down(view_of):
+    """vote-response with a higher term: :follwer, leader-state and leader-id kept (core.clj:130)."""
+    ls = {2: (1, 0), 3: (1, 0)}
+    nodes = {1: node("leader", term=2, leader_id=1, ls=ls), 2: node(), 3: node()}
+    q = {(1, 1): [msg("vote-response", 0, term=5, id=2, vote_granted=False)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(1)
+    r = v.node(1)
+    assert (r["role"], r["current_term"], r["leader_id"], r["ls_present"]) == \
+        (ROLE["follwer"], 5, 1, 1)
+    # append-response with a higher term: leader->follower clears both (core.clj:86-89,145)
+    nodes[1] = node("leader", term=2, leader_id=1, ls=ls, voted_for=0)
+    q = {(1, 1): [msg("append-response", 0, term=4, id=3, success=False)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(1)
+    r = v.node(1)
+    assert (r["role"], r["current_term"], r["leader_id"], r["ls_present"]) == \
+        (ROLE["follower"], 4, 0, 0)
+
+
+def kat_two_leaders_one_term(view_of):
+    """Leader A (term 2, voted-for nil, core.clj:82); a delayed candidate B wins term 2 too."""
+    nodes = {1: node("leader", term=2, leader_id=1, ls={2: (1, 0), 3: (1, 0)}, last_led=2),
+             2: node("candidate", term=2, voted_for=2, votes=[2]),
+             3: node("follwer", term=2, leader_id=1)}
+    q = {(2, 1): [msg("vote-response", 0, term=2, id=3, vote_granted=True)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(1)
+    assert v.node(2)["role"] == ROLE["leader"] and v.node(1)["role"] == ROLE["leader"]
+    c = v.counters()
+    assert c["viol_election"] == 1 and c["leaders"] == 1
+
+
+def kat_vote_rules(view_of):
+    """request-vote-handler (core.clj:91-103): lower term, existing vote, or log mismatch refuse."""
+    nodes = {1: node(term=3, log=[E1], commit=1), 2: node(), 3: node()}
+    q = {(1, 0): [msg("request-vote", 0, term=2, candidate_id=2, last_log_index=0,
+                      last_log_term=None),
+                  msg("request-vote", 0, term=4, candidate_id=3, last_log_index=1,
+                      last_log_term=(9, 9)),
+                  msg("request-vote", 0, term=4, candidate_id=3, last_log_index=1,
+                      last_log_term=E1),
+                  msg("request-vote", 0, term=5, candidate_id=2, last_log_index=0,
+                      last_log_term=None),
+                  msg("request-vote", 0, term=5, candidate_id=2, last_log_index=4,
+                      last_log_term=None)]}
+    v = view_of(Scenario(3, nodes, q))
+    v.step(2)
+    assert v.node(1)["voted_for"] == 0            # stale term, then mismatching entry
+    v.step(1)
+    r = v.node(1)
+    assert r["voted_for"] == 3 and r["current_term"] == 3   # granted, term unchanged
+    v.step(1)
+    assert v.node(1)["voted_for"] == 3            # already voted
+    v.step(1)
+    assert v.node(1)["fault"] == 1                # last-log-index 4 > count: nth throws
+
+
+def kat_variant_no_log_check(view_of):
+    """VOTE_NO_LOG_CHECK skips compare-prev? (core.clj:96,99): no throw, vote granted."""
+    nodes = {1: node(term=1), 2: node()}
+    q = {(1, 0): [msg("request-vote", 0, term=2, candidate_id=2, last_log_index=4,
+                      last_log_term=None)]}
+    scn = Scenario(2, nodes, q, variant_flags=1)
+    v = view_of(scn)
+    v.step(1)
+    assert v.node(1)["fault"] == 0 and v.node(1)["voted_for"] == 2
+
+
+def kat_client_set(view_of):
+    """client-set (core.clj:151-160): leader appends (term, val); others only redirect."""
+    nodes = {1: node("leader", term=4, leader_id=1, ls={2: (1, 0)}), 2: node(term=4)}
+    q = {(1, 0): [msg("client-set", 0, command=77)], (2, 0): [msg("client-set", 0, command=5)]}
+    v = view_of(Scenario(2, nodes, q))
+    v.step(1)
+    assert v.log(1) == [(4, 77)] and v.log(2) == []
+    assert v.node(2)["deadline"] >= 5000          # the event still re-arms the timer
+
+
+ALL = [kat_majority, kat_first_election, kat_duplication, kat_truncate_crash, kat_cce, kat_npe,
+       kat_partial_leader_state, kat_stale_step_down, kat_two_leaders_one_term, kat_vote_rules,
+       kat_variant_no_log_check, kat_client_set]

@@ -1,0 +1,87 @@
+"""The C oracle against the Python restatement (random configs) and the Philox KAT."""
+import ctypes
+import random
+
+import pytest
+
+import helpers
+import pyref
+
+KAT = [((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+       ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD))]
+
+
+@pytest.mark.parametrize("ctr,key,want", KAT)
+def test_philox_kat_python(ctr, key, want):
+    assert pyref.philox(ctr, key) == want
+
+
+@pytest.mark.parametrize("ctr,key,want", KAT)
+def test_philox_kat_c(ctr, key, want):
+    lib = ctypes.CDLL(str(helpers.ORACLE_LIB))
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib.raft_ref_philox(c, k, o)
+    assert tuple(o) == want
+
+
+def random_config(rng):
+    n = rng.choice([2, 3, 4, 5, 5, 5, 6, 7, 8, 9])
+    cfg = dict(nodes=n, seed=rng.getrandbits(64), log_cap=rng.choice([8, 32, 128]),
+               inbox_cap=rng.choice([1, 2, 4, 16]))
+    if rng.random() < 0.7:
+        dmin = rng.randint(1, 5)
+        cfg.update(drop_ppm=rng.choice([0, 50000, 200000]), dup_ppm=rng.choice([0, 20000, 300000]),
+                   dmin=dmin, dmax=dmin + rng.randint(0, 40))
+    if rng.random() < 0.5:
+        cfg.update(part_ppm=rng.choice([50000, 300000]), part_epoch=rng.choice([100, 1000]))
+    cfg["client_ppm"] = rng.choice([0, 100, 1000, 20000])
+    if rng.random() < 0.5:
+        cfg.update(hb=rng.randint(5, 300), el_base=rng.randint(5, 500), el_span=rng.randint(1, 500))
+    if rng.random() < 0.2:
+        cfg["variant_flags"] = 1
+    if rng.random() < 0.3:
+        cfg["arena_cap"] = 2 * cfg["log_cap"]
+    return cfg
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_oracle_equals_python_restatement(seed):
+    rng = random.Random(seed)
+    cfg = random_config(rng)
+    gid = rng.randrange(1 << 20)
+    ticks = 6000
+    be = helpers.oracle(n_clusters=1, cluster_offset=gid, **cfg)
+    pc = pyref.PyCluster(helpers.py_config(**cfg), gid)
+    for chunk in range(3):
+        for t in range(chunk * ticks // 3, (chunk + 1) * ticks // 3):
+            pc.step(t)
+        be.step(ticks // 3)
+        c = be.counters()
+        if c["payload_evicted"]:
+            pytest.skip("arena eviction: the Python restatement models ideal snapshots")
+        helpers.compare_py_backend(pc, be, 0)
+    c = be.counters()
+    for k, v in pc.cnt.items():
+        assert c[k] == v, (k, c[k], v)
+    assert c["first_violation_tick"] == pc.first_violation
+
+
+def test_message_conservation():
+    """sent + client_injected - dropped - partitioned + duplicated = delivered + overflow + to_halted."""
+    be = helpers.oracle(n_clusters=64, nodes=5, seed=5, drop_ppm=100000, dup_ppm=50000, dmax=20,
+                        part_ppm=100000, client_ppm=2000, inbox_cap=3, log_cap=64)
+    be.step(20000)
+    c = be.counters()
+    assert (c["sent"] + c["client_injected"] - c["dropped"] - c["partitioned"] + c["duplicated"]
+            == c["delivered"] + c["overflow"] + c["to_halted"])
+
+
+def test_threads_do_not_change_results():
+    cfg = dict(n_clusters=97, nodes=7, seed=3, client_ppm=1000, drop_ppm=50000, dmax=9)
+    a, b = helpers.oracle(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(b, 5)
+    a.step(7000)
+    b.step(7000)
+    assert (a.digest() == b.digest()).all() and a.counters() == b.counters()
