@@ -86,6 +86,18 @@ struct NodeR {
   uint64_t trace;
 };
 
+// Wave-wide unsigned minimum (all 64 lanes must be active): DPP row shifts build per-row prefix
+// minima, row_bcast15/31 carry them across rows, lane 63 ends with the wave's minimum.
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x111, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x112, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x114, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x118, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x142, 0xa, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
 __device__ __forceinline__ uint32_t wrapq(uint32_t x, uint32_t Q) { return x >= Q ? x - Q : x; }
 
 __device__ __forceinline__ uint32_t* qslots(const DevSim& S, uint32_t gi, int which) {

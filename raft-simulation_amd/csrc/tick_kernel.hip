@@ -59,7 +59,9 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
-template <int N>
+// CLIENT: client-set injection enabled (client_ppm > 0). Without it an idle tick is one scalar
+// compare against the wave's next event tick.
+template <int N, bool CLIENT>
 __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr int CELL_WORDS = CPW * N * N * 8;
@@ -98,12 +100,21 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   }
   uint2* const myar = active ? arena_of(S, gi) : nullptr;
 
+  // Earliest tick at which any lane of the wave can have an event (deadline or queue head);
+  // recomputed after every tick that did work. Idle ticks then cost one scalar compare.
+  auto next_event = [&]() {
+    const uint32_t m = min(n.deadline, min(n.rq.arr, n.rs.arr));
+    return wave_min(active && !n.fault ? m : INF);
+  };
+  uint32_t wnext = next_event();
+
   uint4 cw = make_uint4(0, 0, 0, 0);
   for (uint32_t t = t0; t != t0 + nt; ++t) {
     // ---------------------------------------------------------------- P0 client injection (D9)
+    if (!CLIENT && t < wnext) continue;         // idle tick for every cluster of this wave
     bool inj = false;
     uint32_t injv = 0;
-    if (S.client_ppm) {
+    if (CLIENT) {
       if (t == t0 || (t & 3) == 0) cw = philox(g, P_CLIENT << 8, t >> 2, 0, S.key0, S.key1);
       const uint32_t sel = t & 3;
       const uint32_t wsel = sel == 0 ? cw.x : sel == 1 ? cw.y : sel == 2 ? cw.z : cw.w;
@@ -116,12 +127,13 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         }
       }
     }
+    if (CLIENT && __ballot(inj) == 0 && t < wnext) continue;
     const bool live = active && !n.fault;
-    const bool ev0 = live && (n.rq.arr <= t || n.rs.arr <= t || t >= n.deadline);
-    if (__ballot(ev0 || inj) == 0) continue;  // idle tick for every cluster of this wave
 
-    if (inj) qinsert(S, gi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                     make_uint4(0, 0, 0, 0), lctr);
+    if (CLIENT && __ballot(inj)) {
+      if (inj) qinsert(S, gi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                       make_uint4(0, 0, 0, 0), lctr);
+    }
 
     // ---------------------------------------------------------------- P1 one event per node
     const bool req_ok = live && n.rq.arr <= t;
@@ -138,8 +150,12 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       else if (req_ok) which = 0;
       else if (res_ok) which = 1;
       uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
-      if (which == 0) qpop(S, gi, 0, n.rq, m0, m1);
-      else if (which == 1) qpop(S, gi, 1, n.rs, m0, m1);
+      if (which >= 0) {
+        QueueR q = which ? n.rs : n.rq;
+        qpop(S, gi, which, q, m0, m1);
+        if (which) n.rs = q;
+        else n.rq = q;
+      }
       const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
                      mpoff = m1.w;
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
@@ -357,7 +373,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             transmit<N>(S, g, t, id, src, part, sides, mycells + ((k * N) + src - 1) * 8, ra, rb,
                         sentmask, lctr);
           } else {
-#pragma unroll
+#pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
               if (emit == 2) {
@@ -385,24 +401,30 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
 
     // ---------------------------------------------------------------- P2 network delivery
     if (__ballot(sentmask != 0)) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
+      // copy per loop trip in (sender id, copy) order: a single qinsert call site for the wave.
+      uint32_t inmask = 0;
 #pragma unroll
       for (int s = 0; s < N; ++s) {
         const uint32_t sm = __shfl(sentmask, bl + s);
-        if (active && s != k && ((sm >> id) & 1)) {
-          const uint4* cl = reinterpret_cast<const uint4*>(mycells + (s * N + k) * 8);
-          const uint4 a = cl[0], b = cl[1];
-          const uint32_t copies = b.w >> 16;
-          const uint4 mb0 = make_uint4(t + (b.w & 0xFF), a.x, a.y, a.z);
-          const uint4 mb1 = make_uint4(a.w, b.x, b.y, b.z);
-          const uint4 mc0 = make_uint4(t + ((b.w >> 8) & 0xFF), a.x, a.y, a.z);
-          if ((a.x & 7) <= RAFT_MSG_CLIENT_SET) {
-            qinsert(S, gi, n.fault, 0, n.rq, mb0, mb1, lctr);
-            if (copies == 2) qinsert(S, gi, n.fault, 0, n.rq, mc0, mb1, lctr);
-          } else {
-            qinsert(S, gi, n.fault, 1, n.rs, mb0, mb1, lctr);
-            if (copies == 2) qinsert(S, gi, n.fault, 1, n.rs, mc0, mb1, lctr);
-          }
+        inmask |= ((sm >> id) & 1u) << s;
+      }
+      if (!active) inmask = 0;
+      uint32_t copy = 0;
+      while (inmask) {
+        const int s = __builtin_ctz(inmask);
+        const uint4* cl = reinterpret_cast<const uint4*>(mycells + (s * N + k) * 8);
+        const uint4 a = cl[0], b = cl[1];
+        const uint32_t d = copy == 0 ? (b.w & 0xFF) : ((b.w >> 8) & 0xFF);
+        const int which = (a.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
+        QueueR q = which ? n.rs : n.rq;
+        qinsert(S, gi, n.fault, which, q, make_uint4(t + d, a.x, a.y, a.z),
+                make_uint4(a.w, b.x, b.y, b.z), lctr);
+        if (which) n.rs = q;
+        else n.rq = q;
+        if (++copy >= (b.w >> 16)) {
+          copy = 0;
+          inmask &= inmask - 1;
         }
       }
     }
@@ -509,6 +531,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
       }
     }
+    wnext = next_event();
   }
 
   // ---------------------------------------------------------------- write back
@@ -597,7 +620,10 @@ hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
   constexpr size_t lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
   const uint32_t waves = (S.C + CPW - 1) / CPW;
   const uint32_t blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL(tick_kernel<N>, dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  if (S.client_ppm)
+    hipLaunchKernelGGL((tick_kernel<N, true>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  else
+    hipLaunchKernelGGL((tick_kernel<N, false>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
   return hipGetLastError();
 }
 
@@ -619,7 +645,10 @@ template <int N>
 hipError_t configure_n() {
   constexpr int CPW = 64 / N;
   constexpr int lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, true>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
