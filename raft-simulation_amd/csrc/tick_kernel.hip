@@ -98,7 +98,6 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
     hidx = S.hwm[c * 4]; hterm = S.hwm[c * 4 + 1]; hval = S.hwm[c * 4 + 2];
   }
-  uint2* const myar = active ? arena_of(S, gi) : nullptr;
 
   // Earliest tick at which any lane of the wave can have an event (deadline or queue head);
   // recomputed after every tick that did work. Idle ticks then cost one scalar compare.
@@ -129,9 +128,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     }
     if (CLIENT && __ballot(inj) == 0 && t < wnext) continue;
     const bool live = active && !n.fault;
+    // Opaque per-tick copy of the node index: keeps the compiler from hoisting every address
+    // the event path might use out of the tick loop (that costs ~30 loop-carried VGPRs).
+    uint32_t sgi = gi, sg = g;
+    asm volatile("" : "+v"(sgi), "+v"(sg));
+    uint2* const sar = arena_of(S, sgi);
 
     if (CLIENT && __ballot(inj)) {
-      if (inj) qinsert(S, gi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+      if (inj) qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
                        make_uint4(0, 0, 0, 0), lctr);
     }
 
@@ -144,15 +148,24 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     int appended_at = -1;
     bool elected = false, mchg = false;
     if (live && (req_ok || res_ok || t >= n.deadline)) {
-      const uint4 w = philox(g, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+      // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
+      // and for the next timeout of a non-leader (core.clj:174); leaders' events skip it.
+      uint4 w = make_uint4(0, 0, 0, 0);
+      bool have_w = false;
       int which = -1;
-      if (req_ok && res_ok) which = (w.x & 1) ? 1 : 0;   // alts!! choice, core.clj:181
-      else if (req_ok) which = 0;
-      else if (res_ok) which = 1;
+      if (req_ok && res_ok) {
+        w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+        have_w = true;
+        which = (w.x & 1) ? 1 : 0;
+      } else if (req_ok) {
+        which = 0;
+      } else if (res_ok) {
+        which = 1;
+      }
       uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
       if (which >= 0) {
         QueueR q = which ? n.rs : n.rq;
-        qpop(S, gi, which, q, m0, m1);
+        qpop(S, sgi, which, q, m0, m1);
         if (which) n.rs = q;
         else n.rq = q;
       }
@@ -161,7 +174,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
                      mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
 
-      NodeR nn = n;
+      // Every throw site of the reference precedes every mutation of its handler (SIM_SPEC D8),
+      // so each case decides `fault` first and only then updates the node in place.
       uint32_t fault = 0, ev = 0;
       int emit = 0;                 // 1 request-vote bcast, 2 append-entries bcast, 3 one reply
       int nm = 0;                   // next/match: 1 init, 2 clear, 3 dec next[src], 4 set src
@@ -171,19 +185,26 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       if (which < 0) {
         if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
           ev = 7;
-          emit = 2;
+          // append-entries-rpc (core.clj:56-67): last-entry, then per peer in doseq order
+          // (- nil 1) and subvec of a LazySeq
+          const uint32_t first = id == 1 ? 2u : 1u;
+          if (n.commit > n.len) fault = RAFT_FAULT_IOOBE;
+          else if (!n.lsp || !((n.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
+          else if (n.seq) fault = RAFT_FAULT_CCE;
+          else if ((n.keys & peers) != peers) fault = RAFT_FAULT_NPE;
+          else emit = 2;
         } else {                                            // timeout-handler 166-169
           ev = 6;
-          nn.role = RAFT_CANDIDATE; nn.vf = id; nn.votes = 1u << id; nn.term = n.term + 1;
           if (n.commit > n.len) {                           // last-entry (log.clj:47-49)
             fault = RAFT_FAULT_IOOBE;
           } else {
             uint32_t ep = 0, et = 0, evl = 0;
             if (n.commit) {
-              const uint2 e = myar[(n.base + n.commit - 1) % A];
+              const uint2 e = sar[(n.base + n.commit - 1) % A];
               ep = 1; et = e.x; evl = e.y;
             }
-            ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, nn.term, n.commit, 0);
+            n.role = RAFT_CANDIDATE; n.vf = id; n.votes = 1u << id; n.term += 1;  // 69-73
+            ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, n.term, n.commit, 0);
             rb = make_uint4(et, evl, 0, 0);
             emit = 1;
           }
@@ -196,15 +217,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             if (!(S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) && ma != 0) {
               if (ma > n.len) {
                 fault = RAFT_FAULT_IOOBE;
-              } else {
-                const uint2 e = myar[(n.base + ma - 1) % A];
-                consistent = mep && e.x == met && e.y == mev;
+                break;
               }
+              const uint2 e = sar[(n.base + ma - 1) % A];
+              consistent = mep && e.x == met && e.y == mev;
             }
-            if (fault) break;
             const uint32_t grant = mterm >= n.term && n.vf == 0 && consistent;
-            if (grant) nn.vf = src;
             ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
+            if (grant) n.vf = src;
             emit = 3;
             break;
           }
@@ -215,39 +235,40 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
                 fault = RAFT_FAULT_IOOBE;
                 break;
               }
-              const uint2 e = myar[(n.base + mb - 1) % A];
+              const uint2 e = sar[(n.base + mb - 1) % A];
               consistent = mep && e.x == met && e.y == mev;
             }
             if (mterm < n.term) {
               ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
             } else if (!consistent) {
               ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
-              nn.len = n.len > mb ? n.len - mb : 0;         // remove-from! 78-81
-              nn.seq = 1;
+              n.len = n.len > mb ? n.len - mb : 0;          // remove-from! 78-81
+              n.seq = 1;
             } else {
               if (n.len + pcnt > S.L) {
                 fault = RAFT_FAULT_OVERFLOW;
                 break;
               }
+              ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
               pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff; ppcnt = pcnt;
               pold_base = n.base; pold_len = n.len;
               if (pcnt) {                                    // append-entries! 61-64
                 if (n.base + n.len != n.front) {
                   preloc = 1;
-                  nn.base = n.front;
-                  nn.front = n.front + n.len;
+                  n.base = n.front;
+                  n.front += n.len;
                 }
-                nn.front += pcnt;
+                n.front += pcnt;
                 appended_at = (int)n.len;
               }
-              nn.len = n.len + pcnt;
-              nn.seq = 0;
+              const uint32_t oldc = n.commit;
+              n.len += pcnt;
+              n.seq = 0;
               appended = pcnt;
-              nn.commit = nn.len;                            // apply-entries! 69-76
-              applied = nn.commit > n.commit ? nn.commit - n.commit : 0;
-              ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
-              nn.role = RAFT_FOLLWER; nn.vf = 0; nn.votes = 0;   // candidate->follower 75-78
-              nn.lid = src; nn.term = mterm;
+              n.commit = n.len;                              // apply-entries! 69-76
+              applied = n.commit > oldc ? n.commit - oldc : 0;
+              n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;  // candidate->follower 75-78
+              n.lid = src; n.term = mterm;
             }
             emit = 3;
             break;
@@ -262,14 +283,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             pold_base = n.base; pold_len = n.len;
             if (n.base + n.len != n.front) {
               preloc = 1;
-              nn.base = n.front;
-              nn.front = n.front + n.len;
+              n.base = n.front;
+              n.front += n.len;
             }
-            nn.front += 1;
-            nn.len = n.len + 1;
-            nn.seq = 0;
-            appended = 1;
+            n.front += 1;
             appended_at = (int)n.len;
+            n.len += 1;
+            n.seq = 0;
+            appended = 1;
             break;
           }
           case RAFT_MSG_VOTE_RESPONSE: {                     // vote-response-handler 125-139
@@ -278,15 +299,17 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
               break;
             }
             if (mterm > n.term) {
-              nn.term = mterm;
-              nn.role = RAFT_FOLLWER; nn.vf = 0; nn.votes = 0;
+              n.term = mterm;
+              n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;
             } else if (flag && n.role == RAFT_CANDIDATE) {
               const uint32_t votes = n.votes | 1u << src;
               if (__popc(votes) < (N + 1) / 2) {             // majority? 19-21
-                nn.votes = votes;
+                n.votes = votes;
+              } else if (n.seq) {
+                fault = RAFT_FAULT_CCE;      // append-entries-rpc's entries-from (log.clj:53)
               } else {                                       // candidate->leader 80-84
-                nn.role = RAFT_LEADER; nn.vf = 0; nn.votes = 0; nn.lid = id;
-                nn.lsp = 1; nn.keys = peers;                 // leader-state 40-42
+                n.role = RAFT_LEADER; n.vf = 0; n.votes = 0; n.lid = id;
+                n.lsp = 1; n.keys = peers;                   // leader-state 40-42
                 nm = 1;
                 emit = 2;
                 elected = true;
@@ -296,8 +319,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
           }
           case RAFT_MSG_APPEND_RESPONSE: {                   // append-response-handler 141-149
             if (mterm > n.term) {                            // leader->follower 86-89
-              nn.term = mterm;
-              nn.role = RAFT_FOLLOWER; nn.lid = 0; nn.lsp = 0; nn.keys = 0;
+              n.term = mterm;
+              n.role = RAFT_FOLLOWER; n.lid = 0; n.lsp = 0; n.keys = 0;
               nm = 2;
             } else if (!flag) {
               if (!n.lsp || !((n.keys >> src) & 1)) {
@@ -306,8 +329,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
               }
               nm = 3;
             } else {
-              nn.lsp = 1;
-              nn.keys |= 1u << src;
+              n.lsp = 1;
+              n.keys |= 1u << src;
               nm = 4;
               mchg = true;
             }
@@ -317,17 +340,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             break;
         }
       }
-      // append-entries-rpc (core.clj:56-67) preconditions: last-entry, then per peer (- nil 1)
-      // and subvec-of-LazySeq, in doseq order.
-      if (emit == 2 && !fault) {
-        const uint32_t first = id == 1 ? 2u : 1u;
-        if (nn.commit > nn.len) fault = RAFT_FAULT_IOOBE;
-        else if (!nn.lsp || !((nn.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
-        else if (nn.seq) fault = RAFT_FAULT_CCE;
-        else if ((nn.keys & peers) != peers) fault = RAFT_FAULT_NPE;
-      }
       const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
-      if (fault) {                                   // D8: halt with the pre-event state
+      if (fault) {                                   // D8: halted with the pre-event state
         n.fault = fault;
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
         lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
@@ -336,23 +350,26 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         elected = false;
         mchg = false;
       } else {
-        nn.deadline = nn.role == RAFT_LEADER ? t + S.hb
-                                             : t + S.el_base + __umulhi(w.y, S.el_span);
-        nn.trace = trace_event(n.trace, t, ev, tsrc, tterm, nn.role, nn.term, 0);
+        if (n.role == RAFT_LEADER) {
+          n.deadline = t + S.hb;
+        } else {
+          if (!have_w) w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+          n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
+        }
+        n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
         // leader-state words (cold, in HBM)
         if (nm == 1 || nm == 2) {
 #pragma unroll
           for (int p = 1; p <= N; ++p) {
-            S.next[(p - 1) * NN + gi] = (nm == 1 && p != (int)id) ? (int32_t)(n.commit + 1) : 0;
-            S.match[(p - 1) * NN + gi] = 0;
+            S.next[(p - 1) * NN + sgi] = (nm == 1 && p != (int)id) ? (int32_t)(n.commit + 1) : 0;
+            S.match[(p - 1) * NN + sgi] = 0;
           }
         } else if (nm == 3) {
-          S.next[(src - 1) * NN + gi] -= 1;
+          S.next[(src - 1) * NN + sgi] -= 1;
         } else if (nm == 4) {
-          S.next[(src - 1) * NN + gi] = (int32_t)mb;
-          S.match[(src - 1) * NN + gi] = (int32_t)ma;
+          S.next[(src - 1) * NN + sgi] = (int32_t)mb;
+          S.match[(src - 1) * NN + sgi] = (int32_t)ma;
         }
-        n = nn;
         lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPLIED, applied);
@@ -365,24 +382,24 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
           bool part = false;
           uint32_t sides = 0;
           if (S.part_ppm) {
-            const uint4 pw = philox(g, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
+            const uint4 pw = philox(sg, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
             part = ppm(pw.x) < S.part_ppm;
             sides = pw.y;
           }
           if (emit == 3) {
-            transmit<N>(S, g, t, id, src, part, sides, mycells + ((k * N) + src - 1) * 8, ra, rb,
+            transmit<N>(S, sg, t, id, src, part, sides, mycells + ((k * N) + src - 1) * 8, ra, rb,
                         sentmask, lctr);
           } else {
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
               if (emit == 2) {
-                const int32_t nx = S.next[(p - 1) * NN + gi];
+                const int32_t nx = S.next[(p - 1) * NN + sgi];
                 const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
                 const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
                 uint32_t ep = 0, et = 0, evl = 0, pc = 0, po = 0;
                 if (start < n.len) {
-                  const uint2 e = myar[(n.base + start) % A];
+                  const uint2 e = sar[(n.base + start) % A];
                   ep = 1; et = e.x; evl = e.y;
                   pc = n.len - start - 1;
                   po = pc ? n.base + start + 1 : 0;
@@ -391,7 +408,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
                                 n.commit, (uint32_t)prev);
                 rb = make_uint4(et, evl, po, 0);
               }
-              transmit<N>(S, g, t, id, p, part, sides, mycells + ((k * N) + p - 1) * 8, ra, rb,
+              transmit<N>(S, sg, t, id, p, part, sides, mycells + ((k * N) + p - 1) * 8, ra, rb,
                           sentmask, lctr);
             }
           }
@@ -418,7 +435,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         const uint32_t d = copy == 0 ? (b.w & 0xFF) : ((b.w >> 8) & 0xFF);
         const int which = (a.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
-        qinsert(S, gi, n.fault, which, q, make_uint4(t + d, a.x, a.y, a.z),
+        qinsert(S, sgi, n.fault, which, q, make_uint4(t + d, a.x, a.y, a.z),
                 make_uint4(a.w, b.x, b.y, b.z), lctr);
         if (which) n.rs = q;
         else n.rq = q;
@@ -436,18 +453,18 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       if (pkind != PLAN_NONE && m) {
         if (preloc)
           for (uint32_t i = 0; i < pold_len; ++i)
-            myar[(n.base + i) % A] = myar[(pold_base + i) % A];
+            sar[(n.base + i) % A] = sar[(pold_base + i) % A];
         const uint32_t dst = n.base + pold_len;
         if (pkind == PLAN_ENTRY) {
-          myar[dst % A] = make_uint2(pet, pev);
+          sar[dst % A] = make_uint2(pet, pev);
         } else {
-          const uint2* sa = arena_of(S, c * N + psrc - 1);
+          const uint2* sa = arena_of(S, sgi - k + psrc - 1);
           uint32_t evicted = 0;
           for (uint32_t i = 0; i < m; ++i) {
             uint2 e = make_uint2(0, 0);
             if ((uint64_t)sfront > (uint64_t)ppoff + i + A) ++evicted;
             else e = sa[(ppoff + i) % A];
-            myar[(dst + i) % A] = e;
+            sar[(dst + i) % A] = e;
           }
           lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
         }
@@ -472,10 +489,10 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         for (int s = 0; s < N; ++s) {
           const uint32_t sb = __shfl(n.base, bl + s), sl = __shfl(n.len, bl + s);
           if (appended_at >= 0 && s != k && !bad) {
-            const uint2* oa = arena_of(S, c * N + s);
+            const uint2* oa = arena_of(S, sgi - k + s);
             const uint32_t hi = n.len < sl ? n.len : sl;
             for (uint32_t p = (uint32_t)appended_at; p < hi; ++p) {
-              const uint2 x = myar[(n.base + p) % A], y = oa[(sb + p) % A];
+              const uint2 x = sar[(n.base + p) % A], y = oa[(sb + p) % A];
               if (x.x == y.x && x.y != y.y) {
                 bad = true;
                 break;
@@ -488,7 +505,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       if (elected && hidx > 0) {                     // leader completeness (pre-tick hwm)
         bool ok = n.len >= hidx;
         if (ok) {
-          const uint2 e = myar[(n.base + hidx - 1) % A];
+          const uint2 e = sar[(n.base + hidx - 1) % A];
           ok = e.x == hterm && e.y == hval;
         }
         if (!ok) violation(lctr, RAFT_CTR_VIOL_COMPLETE, t);
@@ -502,7 +519,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
 #pragma unroll
         for (int p = 1; p <= N; ++p) {
           if (p == (int)id) continue;
-          vals[j++] = ((n.keys >> p) & 1) ? S.match[(p - 1) * NN + gi] : 0;
+          vals[j++] = ((n.keys >> p) & 1) ? S.match[(p - 1) * NN + sgi] : 0;
         }
 #pragma unroll
         for (int i = 1; i < N; ++i)
@@ -515,7 +532,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         if (mm > (int32_t)n.len) mm = (int32_t)n.len;
         if (mm > (int32_t)hidx) {
           cm = mm;
-          const uint2 e = myar[(n.base + (uint32_t)mm - 1) % A];
+          const uint2 e = sar[(n.base + (uint32_t)mm - 1) % A];
           ct = e.x; cv = e.y;
         }
       }
