@@ -30,12 +30,17 @@ class Scenario:
     def __init__(self, N, nodes, queues=None, hwm=(0, 0, 0), **cfg):
         self.N, self.nodes, self.hwm = N, nodes, hwm
         self.queues = queues or {}
-        self.cfg = dict(nodes=N, n_clusters=1, log_cap=64, **cfg)
+        self.cfg = dict(dict(nodes=N, n_clusters=1, log_cap=64), **cfg)
 
     # ---------------------------------------------------------------- C ABI backends
     def load_backend(self, make):
         be = make(**self.cfg)
-        recs = be.read_nodes_raw(0, 1)
+        self.load_into(be, 0)
+        return be
+
+    def load_into(self, be, c):
+        """Write this scenario's state into cluster c of an existing backend."""
+        recs = be.read_nodes_raw(c, 1)
         for i in range(1, self.N + 1):
             d, r = self.nodes[i], recs[i - 1]
             r.role, r.current_term = d["role"], d["term"]
@@ -51,13 +56,12 @@ class Scenario:
             for p, (nx, mt) in (d["ls"] or {}).items():
                 r.ls_keys |= 1 << p
                 r.next_index[p - 1], r.match_index[p - 1] = nx, mt
-        be.write_nodes(0, list(recs))
+        be.write_nodes(c, list(recs))
         for i in range(1, self.N + 1):
-            be.write_arena(0, i, self.nodes[i]["log"])
+            be.write_arena(c, i, self.nodes[i]["log"])
         for (i, which), msgs in self.queues.items():
-            be.write_queue(0, i, which, [self._encode(m) for m in msgs])
-        be.write_hwm(0, [self.hwm])
-        return be
+            be.write_queue(c, i, which, [self._encode(m) for m in msgs])
+        be.write_hwm(c, [self.hwm])
 
     def _encode(self, m):
         pm = self._py_msg(m)
