@@ -92,10 +92,13 @@ typedef struct raft_entry {
   uint32_t term, val;
 } raft_entry_t;
 
-/* Cluster record of the leader-completeness checker (SIM_SPEC §4 P4). */
-typedef struct raft_hwm {
-  uint32_t index, term, val, reserved;
-} raft_hwm_t;
+/* Per-cluster record: the leader-completeness checker's high-water mark (SIM_SPEC §4 P4) and the
+ * client-set injection cursor (next injection tick, draws consumed; SIM_SPEC §4 P0). */
+typedef struct raft_cluster {
+  uint32_t hwm_index, hwm_term, hwm_val;
+  uint32_t client_next, client_count;
+  uint32_t reserved[3];
+} raft_cluster_t;
 
 enum raft_counter {
   RAFT_CTR_EV_RV = 0, RAFT_CTR_EV_AE, RAFT_CTR_EV_CS, RAFT_CTR_EV_VR, RAFT_CTR_EV_AR,
@@ -146,8 +149,8 @@ int raft_sim_read_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, raf
 int raft_sim_write_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
                          const raft_entry_t* in, uint32_t count);
 
-int raft_sim_read_hwm(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_hwm_t* out);
-int raft_sim_write_hwm(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_hwm_t* in);
+int raft_sim_read_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_cluster_t* out);
+int raft_sim_write_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_cluster_t* in);
 
 /* Counters of this handle's clusters (no reference counterpart; see SIM_SPEC §4). */
 int raft_sim_read_counters(raft_sim_t* sim, raft_counters_t* out);

@@ -22,7 +22,7 @@ M32 = 0xFFFFFFFF
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
 PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
 
-INIT, EVENT, NET, CLIENT, CLIENT_DETAIL, PART = 1, 2, 3, 4, 5, 6
+INIT, EVENT, NET, CLIENT, PART = 1, 2, 3, 4, 6
 
 
 def philox(ctr, key):
@@ -42,6 +42,28 @@ def philox(ctr, key):
 
 def ppm(w):
     return (w * 1000000) >> 32
+
+
+def client_powers(client_ppm):
+    """pw_i = (1-p)^(2^i) in 32-bit fixed point, truncating (SIM_SPEC §4 P0)."""
+    pw = [((1000000 - client_ppm) << 32) // 1000000]
+    for _ in range(31):
+        pw.append((pw[-1] * pw[-1]) >> 32)
+    return pw
+
+
+def client_gap(w, pw):
+    """Geometric gap: greedy search for the largest G with (1-p)^G >= (w+1)/2^32."""
+    u, acc, g = w + 1, 1 << 32, 0
+    for i in range(31, -1, -1):
+        c = (acc * pw[i]) >> 32
+        if c >= u:
+            acc, g = c, g + (1 << i)
+    return g
+
+
+def sat_tick(x):
+    return x if x < M32 else M32
 
 
 # ----------------------------------------------------------------------------------------------
@@ -364,6 +386,12 @@ class PyCluster:
         self.trace = {i: FNV_OFFSET for i in ids}
         self.last_led = {i: 0 for i in ids}
         self.hwm = (0, 0, 0)
+        self.client_count = 0
+        self.client_next = M32
+        self.client_pw = client_powers(cfg["client_ppm"])
+        if cfg["client_ppm"]:
+            d = philox((gid, CLIENT << 8, 0, 1), self.key)
+            self.client_next = sat_tick(client_gap(d[0], self.client_pw))
         self.cnt = {k: 0 for k in COUNTERS}
         self.first_violation = None
         self.deadline = {}
@@ -420,14 +448,14 @@ class PyCluster:
     # -- one tick --------------------------------------------------------------------------
     def step(self, t):
         cfg, N = self.cfg, self.N
-        # P0 client injection
-        if cfg["client_ppm"]:
-            w = philox((self.gid, CLIENT << 8, t >> 2, 0), self.key)
-            if ppm(w[t & 3]) < cfg["client_ppm"]:
-                d = philox((self.gid, CLIENT_DETAIL << 8, t, 0), self.key)
-                target = 1 + ((d[0] * N) >> 32)
-                self.cnt["client_injected"] += 1
-                self.insert(target, t, {"type": "client-set", "command": d[1]})
+        # P0 client injection: geometric inter-arrival gaps (D9)
+        if t == self.client_next:
+            d = philox((self.gid, CLIENT << 8, self.client_count, 0), self.key)
+            target = 1 + ((d[1] * N) >> 32)
+            self.cnt["client_injected"] += 1
+            self.insert(target, t, {"type": "client-set", "command": d[2]})
+            self.client_count = (self.client_count + 1) & M32
+            self.client_next = sat_tick(t + 1 + client_gap(d[3], self.client_pw))
         sides = self.partition_sides(t)
         outbox = {}
         elected, appended, match_changed = {}, {}, set()
@@ -587,6 +615,10 @@ class PyCluster:
                 "deadline": self.deadline[i] & M32, "next_index": nxt, "match_index": mch,
                 "last_led_term": self.last_led[i], "trace_hash": self.trace[i],
                 "req_count": len(self.req[i]), "res_count": len(self.res[i])}
+
+    def canonical_cluster(self):
+        return {"hwm": tuple(self.hwm), "client_next": self.client_next,
+                "client_count": self.client_count}
 
     def canonical_msgs(self, i, which):
         q = self.req[i] if which == 0 else self.res[i]

@@ -20,7 +20,7 @@ static int fail(int code, const char* msg) {
 const char* raft_ref_last_error(void) { return g_err; }
 
 /* ---------------------------------------------------------------- Philox4x32-10 (SIM_SPEC §5) */
-enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_CLIENT_DETAIL = 5, P_PART = 6 };
+enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 
 void raft_ref_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
@@ -38,6 +38,24 @@ static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, ui
                  uint32_t w[4]);
 static uint32_t ppm(uint32_t w) { return (uint32_t)(((uint64_t)w * 1000000u) >> 32); }
 
+/* pw_i = (1-p)^(2^i) in 32-bit fixed point, truncating (SIM_SPEC §4 P0). */
+static void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
+  pw[0] = ((uint64_t)(1000000u - client_ppm) << 32) / 1000000u;
+  for (int i = 1; i < 32; ++i) pw[i] = (pw[i - 1] * pw[i - 1]) >> 32;
+}
+
+/* Geometric gap: greedy search for the largest G with (1-p)^G >= (w+1)/2^32. */
+static uint64_t client_gap(uint32_t w, const uint64_t pw[32]) {
+  uint64_t u = (uint64_t)w + 1, acc = 1ull << 32, g = 0;
+  for (int i = 31; i >= 0; --i) {
+    uint64_t c = (acc * pw[i]) >> 32;
+    if (c >= u) { acc = c; g += 1ull << i; }
+  }
+  return g;
+}
+
+static uint32_t sat_tick(uint64_t x) { return x < 0xFFFFFFFFull ? (uint32_t)x : 0xFFFFFFFFu; }
+
 /* ---------------------------------------------------------------- FNV-1a-64 over u32 words */
 #define FNV_OFFSET 0xCBF29CE484222325ull
 #define FNV_PRIME 0x100000001B3ull
@@ -52,9 +70,10 @@ struct raft_ref {
   raft_node_t* nodes;   /* [C*N] */
   raft_msg_t* q;        /* [C*N][2][Q], index 0 = head */
   raft_entry_t* arena;  /* [C*N][A] */
-  raft_hwm_t* hwm;      /* [C] */
+  raft_cluster_t* cl;   /* [C] */
   raft_counters_t ctr;
   int threads;
+  uint64_t client_pw[32];
 };
 
 static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
@@ -105,10 +124,17 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
   s->nodes = (raft_node_t*)calloc(nn, sizeof(raft_node_t));
   s->q = (raft_msg_t*)calloc(nn * 2 * s->Q, sizeof(raft_msg_t));
   s->arena = (raft_entry_t*)calloc(nn * s->A, sizeof(raft_entry_t));
-  s->hwm = (raft_hwm_t*)calloc(s->C, sizeof(raft_hwm_t));
-  if (!s->nodes || !s->q || !s->arena || !s->hwm) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+  s->cl = (raft_cluster_t*)calloc(s->C, sizeof(raft_cluster_t));
+  if (!s->nodes || !s->q || !s->arena || !s->cl) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+  client_powers(cfg->client_ppm, s->client_pw);
   for (uint32_t c = 0; c < s->C; ++c) {
     uint32_t g = cfg->cluster_offset + c;
+    s->cl[c].client_next = 0xFFFFFFFFu;
+    if (cfg->client_ppm) {
+      uint32_t d[4];
+      draw(s, g, P_CLIENT << 8, 0, 1, d);
+      s->cl[c].client_next = sat_tick(client_gap(d[0], s->client_pw));
+    }
     for (uint32_t k = 0; k < s->N; ++k) {
       raft_node_t* n = &s->nodes[(size_t)c * s->N + k];
       n->role = RAFT_FOLLOWER;      /* init-node, core.clj:31-38 */
@@ -132,7 +158,7 @@ int raft_ref_set_threads(raft_ref_t* s, int threads) {
 
 void raft_ref_destroy(raft_ref_t* s) {
   if (!s) return;
-  free(s->nodes); free(s->q); free(s->arena); free(s->hwm); free(s);
+  free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s);
 }
 
 uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
@@ -308,18 +334,18 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
   const uint32_t N = s->N;
   uint32_t w[4];
 
-  /* P0 client injection (D9) */
-  if (cfg->client_ppm) {
-    draw(s, x->g, P_CLIENT << 8, t >> 2, 0, w);
-    if (ppm(w[t & 3]) < cfg->client_ppm) {
-      uint32_t d[4];
-      draw(s, x->g, P_CLIENT_DETAIL << 8, t, 0, d);
-      uint32_t target = 1 + (uint32_t)(((uint64_t)d[0] * N) >> 32);
-      raft_msg_t m = {0};
-      m.arrival = t; m.hdr = hdr(RAFT_MSG_CLIENT_SET, 0, 0, 0, 0); m.a = d[1];
-      lc->c[RAFT_CTR_CLIENT_INJECTED]++;
-      queue_insert(x, target - 1, &m);
-    }
+  /* P0 client injection (D9): geometric inter-arrival gaps */
+  raft_cluster_t* cr = &s->cl[c];
+  if (t == cr->client_next) {
+    uint32_t d[4];
+    draw(s, x->g, P_CLIENT << 8, cr->client_count, 0, d);
+    uint32_t target = 1 + (uint32_t)(((uint64_t)d[1] * N) >> 32);
+    raft_msg_t m = {0};
+    m.arrival = t; m.hdr = hdr(RAFT_MSG_CLIENT_SET, 0, 0, 0, 0); m.a = d[2];
+    lc->c[RAFT_CTR_CLIENT_INJECTED]++;
+    queue_insert(x, target - 1, &m);
+    cr->client_count += 1;
+    cr->client_next = sat_tick((uint64_t)t + 1 + client_gap(d[3], s->client_pw));
   }
   x->part = 0; x->sides = 0;
   if (cfg->part_ppm) {
@@ -330,7 +356,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
   plan_t plan[RAFT_MAX_NODES];
   int appended_at[RAFT_MAX_NODES];
   uint32_t elected = 0, match_changed = 0;
-  raft_hwm_t hwm0 = s->hwm[c];
+  const uint32_t h_index = cr->hwm_index, h_term = cr->hwm_term, h_val = cr->hwm_val;
   memset(plan, 0, sizeof plan);
   for (uint32_t k = 0; k < N; ++k) appended_at[k] = -1;
 
@@ -557,7 +583,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
   }
 
   /* P4 invariant checker */
-  if (elected || match_changed || 1) {
+  {
     for (uint32_t k = 0; k < N; ++k) {
       if (!((elected >> k) & 1)) continue;
       uint32_t T = x->nodes[k].last_led_term;
@@ -582,18 +608,18 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
       if (bad) violation(x, RAFT_CTR_VIOL_LOG);
     }
     for (uint32_t k = 0; k < N; ++k) {
-      if (!((elected >> k) & 1) || hwm0.index == 0) continue;
+      if (!((elected >> k) & 1) || h_index == 0) continue;
       const raft_node_t* nk = &x->nodes[k];
       const raft_entry_t* ak = arena_of(s, c * N + k);
-      int ok = nk->log_len >= hwm0.index;
+      int ok = nk->log_len >= h_index;
       if (ok) {
-        raft_entry_t e = ak[(nk->arena_base + hwm0.index - 1) % s->A];
-        ok = e.term == hwm0.term && e.val == hwm0.val;
+        raft_entry_t e = ak[(nk->arena_base + h_index - 1) % s->A];
+        ok = e.term == h_term && e.val == h_val;
       }
       if (!ok) violation(x, RAFT_CTR_VIOL_COMPLETE);
     }
     int32_t best = -1;
-    raft_hwm_t nh = s->hwm[c];
+    uint32_t nh_index = 0, nh_term = 0, nh_val = 0;
     for (uint32_t k = 0; k < N; ++k) {
       const raft_node_t* nk = &x->nodes[k];
       if (nk->role != RAFT_LEADER || !(((elected | match_changed) >> k) & 1)) continue;
@@ -608,13 +634,13 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
         }
       int32_t mm = vals[(N + 1) / 2 - 1];
       if (mm > (int32_t)nk->log_len) mm = (int32_t)nk->log_len;
-      if (mm > (int32_t)s->hwm[c].index && mm > best) {
+      if (mm > (int32_t)h_index && mm > best) {
         best = mm;
         raft_entry_t e = arena_of(s, c * N + k)[(nk->arena_base + (uint32_t)mm - 1) % s->A];
-        nh.index = (uint32_t)mm; nh.term = e.term; nh.val = e.val;
+        nh_index = (uint32_t)mm; nh_term = e.term; nh_val = e.val;
       }
     }
-    if (best > 0) s->hwm[c] = nh;
+    if (best > 0) { cr->hwm_index = nh_index; cr->hwm_term = nh_term; cr->hwm_val = nh_val; }
   }
 }
 
@@ -762,18 +788,18 @@ int raft_ref_write_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, const raf
   return 0;
 }
 
-int raft_ref_read_hwm(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_hwm_t* out) {
+int raft_ref_read_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
-  memcpy(out, s->hwm + c0, nc * sizeof *out);
+  memcpy(out, s->cl + c0, nc * sizeof *out);
   return 0;
 }
 
-int raft_ref_write_hwm(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_hwm_t* in) {
+int raft_ref_write_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
-  memcpy(s->hwm + c0, in, nc * sizeof *in);
-  for (uint32_t i = 0; i < nc; ++i) s->hwm[c0 + i].reserved = 0;
+  memcpy(s->cl + c0, in, nc * sizeof *in);
+  for (uint32_t i = 0; i < nc; ++i) memset(s->cl[c0 + i].reserved, 0, sizeof in->reserved);
   return 0;
 }
 
@@ -819,9 +845,11 @@ int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
         h = fnv(h, e.val);
       }
     }
-    h = fnv(h, s->hwm[c].index);
-    h = fnv(h, s->hwm[c].term);
-    h = fnv(h, s->hwm[c].val);
+    h = fnv(h, s->cl[c].hwm_index);
+    h = fnv(h, s->cl[c].hwm_term);
+    h = fnv(h, s->cl[c].hwm_val);
+    h = fnv(h, s->cl[c].client_next);
+    h = fnv(h, s->cl[c].client_count);
     out[ci] = h;
   }
   return 0;

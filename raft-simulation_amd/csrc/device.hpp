@@ -6,7 +6,7 @@
 //   cold node words  next_index / match_index                              [N][NN] i32
 //   queues           qbuf[gi][which][Q] of 8-word messages (ring, sorted by arrival)
 //   log arenas       arena[gi][A] of (term, val)
-//   cluster words    hwm[c] = (index, term, val, 0)
+//   cluster words    cl[c] = raft_cluster_t (hwm index, term, val, client_next, client_count, 0,0,0)
 // A wave owns floor(64 / N) whole clusters, one lane per node; a cluster never spans waves, so all
 // intra-cluster traffic is lane-to-lane inside one wave (LDS cells + ds_bpermute).
 #pragma once
@@ -18,10 +18,11 @@
 namespace rs {
 
 constexpr uint32_t INF = 0xFFFFFFFFu;
-enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_CLIENT_DETAIL = 5, P_PART = 6 };
+enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;  // per-wave LDS counter slot holding min tick
 constexpr int LCTR_WORDS = 32;
+constexpr int PW_WORDS = 64;   // 32 x u64 client-gap powers at the start of the block's LDS
 
 struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
@@ -32,7 +33,9 @@ struct DevSim {
   int32_t *next, *match;  // [N][NN], row p-1 for peer id p
   uint32_t* qbuf;         // [NN][2][Q][8]
   uint32_t* arena;        // [NN][A][2]
-  uint32_t* hwm;          // [C][4]
+  uint32_t* cl;           // [C][8] raft_cluster_t
+  const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
+  int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)
 };
 
@@ -54,6 +57,29 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
 }
 
 __device__ __forceinline__ uint32_t ppm(uint32_t w) { return __umulhi(w, 1000000u); }
+
+// pw_i = (1-p)^(2^i) in 32-bit fixed point, truncating (SIM_SPEC §4 P0); computed on the host.
+inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
+  pw[0] = ((uint64_t)(1000000u - client_ppm) << 32) / 1000000u;
+  for (int i = 1; i < 32; ++i) pw[i] = (pw[i - 1] * pw[i - 1]) >> 32;
+}
+
+// Tick of the next client-set after tick t (t = -1 for the first): t + 1 + G(w), where G is the
+// greedy power search of SIM_SPEC §4 P0 over pw[top..0] (higher powers are 0 and never fire).
+__device__ inline uint32_t client_next_tick(int64_t t, uint32_t w, const unsigned long long* pw,
+                                            int top) {
+  const uint64_t u = (uint64_t)w + 1;
+  uint64_t acc = 1ull << 32, g = 0;
+  for (int i = top; i >= 0; --i) {
+    const uint64_t c = (acc * pw[i]) >> 32;
+    if (c >= u) {
+      acc = c;
+      g += 1ull << i;
+    }
+  }
+  const uint64_t nx = (uint64_t)(t + 1) + g;
+  return nx < 0xFFFFFFFFull ? (uint32_t)nx : 0xFFFFFFFFu;
+}
 
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;

@@ -42,6 +42,7 @@ struct raft_sim {
   std::vector<void*> allocs;
   double last_ms;
   uint32_t last_launches;
+  unsigned long long* client_pw;
 };
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -125,6 +126,12 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   d.drop_ppm = cfg->drop_ppm; d.dup_ppm = cfg->dup_ppm; d.dmin = cfg->dmin; d.dmax = cfg->dmax;
   d.part_ppm = cfg->part_ppm; d.part_epoch = cfg->part_epoch; d.client_ppm = cfg->client_ppm;
   d.variant = cfg->variant_flags;
+  uint64_t pw[32];
+  rs::client_powers(cfg->client_ppm, pw);
+  d.client_pw = nullptr;
+  d.client_top = -1;
+  for (int i = 0; i < 32; ++i)
+    if (pw[i]) d.client_top = i;
   const size_t NN = s->NN;
   uint32_t** hot[] = {&d.flags, &d.masks, &d.term, &d.commit, &d.len, &d.deadline, &d.qmeta,
                       &d.req_arr, &d.res_arr, &d.req_tail, &d.res_tail, &d.abase, &d.afront,
@@ -133,11 +140,12 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
     if ((rc = dalloc(s, p, NN))) { raft_sim_destroy(s); return rc; }
   if ((rc = dalloc(s, &d.next, NN * s->N)) || (rc = dalloc(s, &d.match, NN * s->N)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
-      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.hwm, (size_t)s->C * 4)) ||
-      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1))) {
+      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.cl, (size_t)s->C * 8)) ||
+      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1)) || (rc = dalloc(s, &s->client_pw, 32))) {
     raft_sim_destroy(s);
     return rc;
   }
+  d.client_pw = s->client_pw;
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreate(&s->ev_start)) != hipSuccess ||
@@ -146,9 +154,10 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (e = hipMemsetAsync(d.match, 0, NN * s->N * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
-      (e = hipMemsetAsync(d.hwm, 0, (size_t)s->C * 16, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
+          hipSuccess ||
       (e = rs::launch_init(d, s->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
     raft_sim_destroy(s);
@@ -380,23 +389,24 @@ int raft_sim_write_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, const raf
   return 0;
 }
 
-int raft_sim_read_hwm(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_hwm_t* out) {
+int raft_sim_read_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
-  HIP_OK(hipMemcpyAsync(out, s->d.hwm + (size_t)c0 * 4, nc * sizeof(raft_hwm_t),
+  static_assert(sizeof(raft_cluster_t) == 32, "cluster record is 8 words");
+  HIP_OK(hipMemcpyAsync(out, s->d.cl + (size_t)c0 * 8, nc * sizeof(raft_cluster_t),
                         hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }
 
-int raft_sim_write_hwm(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_hwm_t* in) {
+int raft_sim_write_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
-  std::vector<raft_hwm_t> buf(in, in + nc);
-  for (auto& h : buf) h.reserved = 0;
-  HIP_OK(hipMemcpyAsync(s->d.hwm + (size_t)c0 * 4, buf.data(), nc * sizeof(raft_hwm_t),
+  std::vector<raft_cluster_t> buf(in, in + nc);
+  for (auto& h : buf) h.reserved[0] = h.reserved[1] = h.reserved[2] = 0;
+  HIP_OK(hipMemcpyAsync(s->d.cl + (size_t)c0 * 8, buf.data(), nc * sizeof(raft_cluster_t),
                         hipMemcpyHostToDevice, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;

@@ -59,9 +59,7 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
-// CLIENT: client-set injection enabled (client_ppm > 0). Without it an idle tick is one scalar
-// compare against the wave's next event tick.
-template <int N, bool CLIENT>
+template <int N>
 __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr int CELL_WORDS = CPW * N * N * 8;
@@ -69,7 +67,11 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* cells = smem + wv * WAVE_WORDS;
+  // block-shared: the client-gap power table (SIM_SPEC P0), then one region per wave
+  unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
+  if (threadIdx.x < 32) pw[threadIdx.x] = S.client_pw[threadIdx.x];
+  __syncthreads();
+  uint32_t* cells = smem + PW_WORDS + wv * WAVE_WORDS;
   uint32_t* lctr = cells + CELL_WORDS;
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
@@ -84,7 +86,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   uint32_t* mycells = cells + (cs < CPW ? cs : 0) * N * N * 8;
 
   NodeR n = {};
-  uint32_t hidx = 0, hterm = 0, hval = 0;
+  uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
+  uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
   if (active) {
     const uint32_t fl = S.flags[gi], mk = S.masks[gi], qm = S.qmeta[gi];
     n.role = fl & 3; n.vf = (fl >> 2) & 15; n.lid = (fl >> 6) & 15; n.fault = (fl >> 10) & 7;
@@ -96,37 +99,20 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     n.rq.tail = S.req_tail[gi]; n.rs.tail = S.res_tail[gi];
     n.base = S.abase[gi]; n.front = S.afront[gi]; n.led = S.led[gi];
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
-    hidx = S.hwm[c * 4]; hterm = S.hwm[c * 4 + 1]; hval = S.hwm[c * 4 + 2];
+    hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
+    cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
   }
 
   // Earliest tick at which any lane of the wave can have an event (deadline or queue head);
   // recomputed after every tick that did work. Idle ticks then cost one scalar compare.
   auto next_event = [&]() {
-    const uint32_t m = min(n.deadline, min(n.rq.arr, n.rs.arr));
-    return wave_min(active && !n.fault ? m : INF);
+    const uint32_t m = n.fault ? INF : min(n.deadline, min(n.rq.arr, n.rs.arr));
+    return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
 
-  uint4 cw = make_uint4(0, 0, 0, 0);
   for (uint32_t t = t0; t != t0 + nt; ++t) {
-    // ---------------------------------------------------------------- P0 client injection (D9)
-    if (!CLIENT && t < wnext) continue;         // idle tick for every cluster of this wave
-    bool inj = false;
-    uint32_t injv = 0;
-    if (CLIENT) {
-      if (t == t0 || (t & 3) == 0) cw = philox(g, P_CLIENT << 8, t >> 2, 0, S.key0, S.key1);
-      const uint32_t sel = t & 3;
-      const uint32_t wsel = sel == 0 ? cw.x : sel == 1 ? cw.y : sel == 2 ? cw.z : cw.w;
-      if (active && ppm(wsel) < S.client_ppm) {
-        const uint4 d = philox(g, P_CLIENT_DETAIL << 8, t, 0, S.key0, S.key1);
-        if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
-        if (1 + __umulhi(d.x, N) == id) {
-          inj = true;
-          injv = d.y;
-        }
-      }
-    }
-    if (CLIENT && __ballot(inj) == 0 && t < wnext) continue;
+    if (t < wnext) continue;                   // idle tick for every cluster of this wave
     const bool live = active && !n.fault;
     // Opaque per-tick copy of the node index: keeps the compiler from hoisting every address
     // the event path might use out of the tick loop (that costs ~30 loop-carried VGPRs).
@@ -134,13 +120,37 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     asm volatile("" : "+v"(sgi), "+v"(sg));
     uint2* const sar = arena_of(S, sgi);
 
-    if (CLIENT && __ballot(inj)) {
-      if (inj) qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                       make_uint4(0, 0, 0, 0), lctr);
+    // ---------------------------------------------------------------- P0 client injection (D9)
+    bool inj = false;
+    uint32_t injv = 0;
+    const bool cinj = active && t == cnext;
+    if (__ballot(cinj)) {
+      if (cinj) {
+        const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
+        if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
+        if (1 + __umulhi(d.y, N) == id) {
+          inj = true;
+          injv = d.z;
+        }
+        ccount += 1;
+        cnext = client_next_tick(t, d.w, pw, S.client_top);
+      }
+    }
+
+    // A client-set that lands in an empty REQ queue would be its head at arrival t, so it is
+    // kept in registers (dcs) instead of a global store + same-tick load; it is written to the
+    // queue only if this tick's alts!! choice takes the RES queue instead.
+    bool dcs = false;
+    if (__ballot(inj)) {
+      if (inj) {
+        if (live && n.rq.c == 0) dcs = true;
+        else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                     make_uint4(0, 0, 0, 0), lctr);
+      }
     }
 
     // ---------------------------------------------------------------- P1 one event per node
-    const bool req_ok = live && n.rq.arr <= t;
+    const bool req_ok = live && (dcs || n.rq.arr <= t);
     const bool res_ok = live && n.rs.arr <= t;
     uint32_t sentmask = 0;
     uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, pold_len = 0,
@@ -163,7 +173,16 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         which = 1;
       }
       uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
-      if (which >= 0) {
+      if (dcs) {
+        if (which == 0) {
+          m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
+          lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+        } else {
+          qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                  make_uint4(0, 0, 0, 0), lctr);
+        }
+      }
+      if (which >= 0 && !(dcs && which == 0)) {
         QueueR q = which ? n.rs : n.rq;
         qpop(S, sgi, which, q, m0, m1);
         if (which) n.rs = q;
@@ -451,20 +470,32 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
       if (pkind != PLAN_NONE && m) {
-        if (preloc)
-          for (uint32_t i = 0; i < pold_len; ++i)
-            sar[(n.base + i) % A] = sar[(pold_base + i) % A];
-        const uint32_t dst = n.base + pold_len;
+        // physical slots advance with a wrap instead of a per-entry modulo
+        if (preloc) {
+          uint32_t si = pold_base % A, di = n.base % A;
+          for (uint32_t i = 0; i < pold_len; ++i) {
+            sar[di] = sar[si];
+            si = si + 1 == A ? 0 : si + 1;
+            di = di + 1 == A ? 0 : di + 1;
+          }
+        }
+        uint32_t di = (n.base + pold_len) % A;
         if (pkind == PLAN_ENTRY) {
-          sar[dst % A] = make_uint2(pet, pev);
+          sar[di] = make_uint2(pet, pev);
         } else {
+          // entries i with sender frontier > poff + i + A were overwritten (SIM_SPEC P3)
+          const int64_t ev = (int64_t)sfront - (int64_t)A - (int64_t)ppoff;
+          const uint32_t evicted = ev <= 0 ? 0u : (ev >= (int64_t)m ? m : (uint32_t)ev);
           const uint2* sa = arena_of(S, sgi - k + psrc - 1);
-          uint32_t evicted = 0;
-          for (uint32_t i = 0; i < m; ++i) {
-            uint2 e = make_uint2(0, 0);
-            if ((uint64_t)sfront > (uint64_t)ppoff + i + A) ++evicted;
-            else e = sa[(ppoff + i) % A];
-            sar[(dst + i) % A] = e;
+          uint32_t si = (ppoff + evicted) % A;
+          for (uint32_t i = 0; i < evicted; ++i) {
+            sar[di] = make_uint2(0, 0);
+            di = di + 1 == A ? 0 : di + 1;
+          }
+          for (uint32_t i = evicted; i < m; ++i) {
+            sar[di] = sa[si];
+            si = si + 1 == A ? 0 : si + 1;
+            di = di + 1 == A ? 0 : di + 1;
           }
           lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
         }
@@ -562,7 +593,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
     S.trace_lo[gi] = (uint32_t)n.trace; S.trace_hi[gi] = (uint32_t)(n.trace >> 32);
     if (k == 0) {
-      S.hwm[c * 4] = hidx; S.hwm[c * 4 + 1] = hterm; S.hwm[c * 4 + 2] = hval;
+      S.cl[c * 8] = hidx; S.cl[c * 8 + 1] = hterm; S.cl[c * 8 + 2] = hval;
+      S.cl[c * 8 + 3] = cnext; S.cl[c * 8 + 4] = ccount;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -586,6 +618,15 @@ __global__ void init_kernel(DevSim S) {
   S.qmeta[gi] = 0; S.req_arr[gi] = INF; S.res_arr[gi] = INF; S.req_tail[gi] = 0;
   S.res_tail[gi] = 0; S.abase[gi] = 0; S.afront[gi] = 0; S.led[gi] = 0;
   S.trace_lo[gi] = 0x84222325u; S.trace_hi[gi] = 0xCBF29CE4u;
+  if (id == 1) {                                   // cluster record: no hwm, first client-set
+    uint32_t first = INF;
+    if (S.client_ppm) {
+      const uint4 d = philox(S.goff + c, P_CLIENT << 8, 0, 1, S.key0, S.key1);
+      first = client_next_tick(-1, d.x, S.client_pw, S.client_top);
+    }
+    for (int i = 0; i < 8; ++i) S.cl[c * 8 + i] = 0;
+    S.cl[c * 8 + 3] = first;
+  }
 }
 
 // Per-cluster canonical digest (SIM_SPEC §6), one thread per cluster.
@@ -625,22 +666,17 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       h = fnv(h, e.y);
     }
   }
-  h = fnv(h, S.hwm[c * 4]);
-  h = fnv(h, S.hwm[c * 4 + 1]);
-  h = fnv(h, S.hwm[c * 4 + 2]);
+  for (int i = 0; i < 5; ++i) h = fnv(h, S.cl[c * 8 + i]);
   out[ci] = h;
 }
 
 template <int N>
 hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
   constexpr int CPW = 64 / N;
-  constexpr size_t lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
+  constexpr size_t lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
   const uint32_t waves = (S.C + CPW - 1) / CPW;
   const uint32_t blocks = (waves + 3) / 4;
-  if (S.client_ppm)
-    hipLaunchKernelGGL((tick_kernel<N, true>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
-  else
-    hipLaunchKernelGGL((tick_kernel<N, false>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  hipLaunchKernelGGL(tick_kernel<N>, dim3(blocks), dim3(256), lds, st, S, t0, nt);
   return hipGetLastError();
 }
 
@@ -661,11 +697,8 @@ hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st
 template <int N>
 hipError_t configure_n() {
   constexpr int CPW = 64 / N;
-  constexpr int lds = 4 * (CPW * N * N * 8 + LCTR_WORDS) * sizeof(uint32_t);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, false>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, true>),
+  constexpr int lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 

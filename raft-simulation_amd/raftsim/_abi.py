@@ -61,9 +61,14 @@ class Entry(C.Structure):
     _fields_ = [("term", C.c_uint32), ("val", C.c_uint32)]
 
 
-class Hwm(C.Structure):
-    _fields_ = [("index", C.c_uint32), ("term", C.c_uint32), ("val", C.c_uint32),
-                ("reserved", C.c_uint32)]
+class Cluster(C.Structure):
+    _fields_ = [("hwm_index", C.c_uint32), ("hwm_term", C.c_uint32), ("hwm_val", C.c_uint32),
+                ("client_next", C.c_uint32), ("client_count", C.c_uint32),
+                ("reserved", C.c_uint32 * 3)]
+
+    def as_dict(self):
+        return {"hwm": (self.hwm_index, self.hwm_term, self.hwm_val),
+                "client_next": self.client_next, "client_count": self.client_count}
 
 
 class Counters(C.Structure):
@@ -93,8 +98,8 @@ _SIGS = {
                               C.c_uint32]),
     "read_arena": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Entry), C.c_uint32]),
     "write_arena": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Entry), C.c_uint32]),
-    "read_hwm": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Hwm)]),
-    "write_hwm": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Hwm)]),
+    "read_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
+    "write_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
     "read_counters": (C.c_int, [C.c_void_p, P(Counters)]),
     "digest": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint64)]),
     "last_step_timing": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32)]),

@@ -133,17 +133,19 @@ class Backend:
         A = len(ar)
         return [ar[(rec["arena_base"] + i) % A] for i in range(rec["log_len"])]
 
-    def read_hwm(self, c0=0, nc=None):
+    def read_clusters(self, c0=0, nc=None):
+        """Per-cluster records: checker high-water mark and client-injection cursor."""
         nc = self.C - c0 if nc is None else nc
-        arr = (_abi.Hwm * nc)()
-        self._check(self._fns["read_hwm"](self._h, c0, nc, arr))
-        return [(h.index, h.term, h.val) for h in arr]
+        arr = (_abi.Cluster * nc)()
+        self._check(self._fns["read_clusters"](self._h, c0, nc, arr))
+        return [r.as_dict() for r in arr]
 
-    def write_hwm(self, c0, hwms):
-        arr = (_abi.Hwm * len(hwms))()
-        for i, (a, b, c) in enumerate(hwms):
-            arr[i].index, arr[i].term, arr[i].val = a, b, c
-        self._check(self._fns["write_hwm"](self._h, c0, len(hwms), arr))
+    def write_clusters(self, c0, recs):
+        arr = (_abi.Cluster * len(recs))()
+        for i, r in enumerate(recs):
+            arr[i].hwm_index, arr[i].hwm_term, arr[i].hwm_val = r["hwm"]
+            arr[i].client_next, arr[i].client_count = r["client_next"], r["client_count"]
+        self._check(self._fns["write_clusters"](self._h, c0, len(recs), arr))
 
     def counters(self):
         c = _abi.Counters()

@@ -10,6 +10,6 @@ for l in sys.stdin:
     m=re.search(r'(VGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)',l)
     if m and name and 'tick' in name:
         row.setdefault(name,[]).append(m.group(2))
-for k,v in row.items(): print(re.search(r'ILi(\d)ELb(\d)',k).groups(), 'vgpr/scratch/occ', v)
+for k,v in row.items(): print(re.search(r'ILi(\d)',k).group(1), 'vgpr/scratch/occ', v)
 "
-awk '/^_ZN2rs11tick_kernelILi5ELb0EEEvNS_6DevSimEjj:/,/s_endpgm/' /tmp/tick_kernel-hip-amdgcn-amd-amdhsa-gfx950.s > /tmp/k5.s
+awk '/^_ZN2rs11tick_kernelILi5EEEvNS_6DevSimEjj:/,/s_endpgm/' /tmp/tick_kernel-hip-amdgcn-amd-amdhsa-gfx950.s > /tmp/k5.s

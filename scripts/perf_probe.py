@@ -16,6 +16,8 @@ PROBES = {
     "c2_q4": dict(n_clusters=65536, nodes=5, seed=42, inbox_cap=4),
     "c3": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=10000, log_cap=256, **FAULTS),
     "c3_lowclient": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=200, log_cap=256, **FAULTS),
+    "c2_client1": dict(n_clusters=65536, nodes=5, seed=42, client_ppm=1),
+    "c3_noclient": dict(n_clusters=131072, nodes=5, seed=1, log_cap=256, **FAULTS),
     "c4_n9": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=250000, log_cap=4096),
 }
 

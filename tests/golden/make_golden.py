@@ -57,7 +57,8 @@ def make(name, spec):
         n["res"] = [list(m[:7]) + [[list(e) for e in m[7]]] for m in c.canonical_msgs(i, 1)]
         nodes.append(n)
     out = {"config": spec["cfg"], "cluster_offset": spec["gid"], "ticks": spec["ticks"],
-           "nodes": nodes, "hwm": list(c.hwm), "counters": c.cnt,
+           "nodes": nodes, "hwm": list(c.hwm), "client": [c.client_next, c.client_count],
+           "counters": c.cnt,
            "first_violation_tick": c.first_violation}
     if spec["trace"]:
         out["events"] = c.events

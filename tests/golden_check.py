@@ -47,7 +47,9 @@ def check(name, make):
                     ar = be.read_arena(0, (m[1] >> 3) & 15)
                     got_p = [list(ar[(m[7] + k) % len(ar)]) for k in range(pcnt)]
                     assert got_p == w[7], (name, i + 1, "payload")
-    assert list(be.read_hwm(0, 1)[0]) == fx["hwm"]
+    cr = be.read_clusters(0, 1)[0]
+    assert list(cr["hwm"]) == fx["hwm"]
+    assert [cr["client_next"], cr["client_count"]] == fx["client"]
     c = be.counters()
     for k, v in fx["counters"].items():
         assert c[k] == v, (name, k, c[k], v)

@@ -49,7 +49,7 @@ def compare_py_backend(pc: "pyref.PyCluster", be: Backend, cluster: int):
                     ar = be.read_arena(cluster, src)
                     A = len(ar)
                     assert [ar[(g[7] + k) % A] for k in range(pcnt)] == [tuple(e) for e in w[7]]
-    assert be.read_hwm(cluster, 1)[0] == tuple(pc.hwm)
+    assert be.read_clusters(cluster, 1)[0] == pc.canonical_cluster()
 
 
 def gpu(**cfg):
@@ -80,9 +80,9 @@ def describe_cluster_diff(a, b, cluster):
         la, lb = a.log(cluster, i + 1), b.log(cluster, i + 1)
         if la != lb:
             lines.append(f"  node {i + 1} log: {la[:12]}... != {lb[:12]}...")
-    ha, hb = a.read_hwm(cluster, 1), b.read_hwm(cluster, 1)
+    ha, hb = a.read_clusters(cluster, 1), b.read_clusters(cluster, 1)
     if ha != hb:
-        lines.append(f"  hwm {ha} != {hb}")
+        lines.append(f"  cluster record {ha} != {hb}")
     return "\n".join(lines)
 
 

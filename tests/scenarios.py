@@ -61,7 +61,9 @@ class Scenario:
             be.write_arena(c, i, self.nodes[i]["log"])
         for (i, which), msgs in self.queues.items():
             be.write_queue(c, i, which, [self._encode(m) for m in msgs])
-        be.write_hwm(c, [self.hwm])
+        rec = be.read_clusters(c, 1)[0]
+        rec["hwm"] = tuple(self.hwm)
+        be.write_clusters(c, [rec])
 
     def _encode(self, m):
         pm = self._py_msg(m)

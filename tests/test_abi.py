@@ -45,7 +45,7 @@ def test_oracle_mirrors_the_abi():
 
 def test_struct_layouts_match_the_c_compiler(tmp_path):
     structs = {"raft_sim_config_t": _abi.Config, "raft_node_t": _abi.Node,
-               "raft_msg_t": _abi.Msg, "raft_entry_t": _abi.Entry, "raft_hwm_t": _abi.Hwm,
+               "raft_msg_t": _abi.Msg, "raft_entry_t": _abi.Entry, "raft_cluster_t": _abi.Cluster,
                "raft_counters_t": _abi.Counters}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"',
              "int main(void) {"]

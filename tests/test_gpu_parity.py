@@ -109,7 +109,7 @@ def test_gpu_write_state_roundtrip():
     r = helpers.oracle(**cfg)
     for be in (g, r):
         be.write_nodes(0, src.read_nodes_raw())
-        be.write_hwm(0, src.read_hwm())
+        be.write_clusters(0, src.read_clusters())
         for c in range(cfg["n_clusters"]):
             for i in range(1, 6):
                 be.write_arena(c, i, src.read_arena(c, i))
