@@ -8,9 +8,11 @@ cites the reference line it restates. AppendEntries payloads are real copies tak
 ideal snapshot semantics); the C oracle and the kernel reference the sender's log arena instead and
 agree with this module whenever their `payload_evicted` counter is 0.
 
-Parity status: the reference ships no tests or golden vectors and needs a JVM that
-this image lacks, so this restatement is pinned by the hand-derived known-answer tests in
-tests/test_kat.py (each derived from the cited source lines) and by the Random123 Philox vectors.
+Parity status: PARITY UNPINNED by the reference. The reference ships no tests, fixtures or golden
+vectors and cannot run here (Clojure 1.6 on a JVM; no JVM in this image). What
+pins this restatement instead: the hand-derived known-answer scenarios of tests/scenarios.py (each
+cites the source lines it derives from), the Random123 Philox4x32-10 vectors, and field-for-field
+agreement with the independently written C oracle (tests/test_oracle.py, tests/test_fuzz.py).
 """
 from __future__ import annotations
 

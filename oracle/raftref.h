@@ -7,9 +7,11 @@
  * ABI with the raft_ref_ prefix, plus raft_ref_set_threads (the pmap analogue for the CPU
  * baseline: clusters are split into contiguous chunks, one std thread each).
  *
- * Parity status: pinned by hand-derived KATs (tests/test_kat.py) and the Random123 Philox vectors,
- * and cross-checked against the independent Python restatement oracle/pyref.py. The reference
- * itself cannot run here (Clojure 1.6 on a JVM that this image lacks: SURVEY.md §8c).
+ * Parity status: PARITY UNPINNED by the reference, which ships no tests or golden vectors and
+ * cannot run here (Clojure 1.6 on a JVM that this image lacks: SURVEY.md §8c). Pinned instead by
+ * hand-derived known-answer scenarios (tests/scenarios.py, each citing its source lines), the
+ * Random123 Philox vectors, and agreement with the independent Python restatement oracle/pyref.py
+ * on random configurations and random states (tests/test_oracle.py, tests/test_fuzz.py).
  */
 #ifndef RAFTREF_H
 #define RAFTREF_H
