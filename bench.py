@@ -72,8 +72,8 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--clusters", type=int, default=CLUSTERS_PER_GPU)
     ap.add_argument("--ticks-per-launch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -62,7 +62,8 @@ typedef struct raft_sim_config {
   uint32_t variant_flags;
   int32_t device;            /* HIP device ordinal */
   uint32_t ticks_per_launch; /* ticks fused into one kernel launch; 0 -> default */
-  uint32_t reserved[4];
+  uint32_t commit_stream_cap; /* per-node ring of committed :val's (log.clj:69-76); 0 = off */
+  uint32_t reserved[3];
 } raft_sim_config_t;
 
 /* Canonical node record: the node map of init-node (core.clj:31-38) plus the log atom
@@ -79,7 +80,7 @@ typedef struct raft_node {
   uint32_t last_led_term;
   uint32_t arena_base, arena_frontier;
   uint32_t req_count, res_count; /* read-only: set through raft_sim_write_queue */
-  uint32_t reserved1;
+  uint32_t commit_count;         /* lines apply-entries! has written to node_<id>.log so far */
   uint64_t trace_hash;
 } raft_node_t;
 
@@ -148,6 +149,14 @@ int raft_sim_read_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, raf
                         uint32_t cap);
 int raft_sim_write_arena(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
                          const raft_entry_t* in, uint32_t count);
+
+/* F2: the newest min(count, commit_stream_cap, cap) values apply-entries! wrote to node_<id>.log
+ * (log.clj:16-18,69-76), oldest first; returns how many were copied. write_commit_stream stores
+ * `count` values as the newest ones ending at the node record's commit_count. */
+int raft_sim_read_commit_stream(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
+                                uint32_t* out, uint32_t cap);
+int raft_sim_write_commit_stream(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
+                                 const uint32_t* in, uint32_t count);
 
 int raft_sim_read_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_cluster_t* out);
 int raft_sim_write_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_cluster_t* in);

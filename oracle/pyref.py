@@ -256,7 +256,9 @@ def append_entries_handler(log, message, node, respond, stats):     # core.clj:1
     stats["appended_at"] = len(log.entries)
     append_entries(log, message["entries"])
     stats["entries_appended"] += len(message["entries"])
-    stats["entries_applied"] += apply_entries(log)
+    amount = apply_entries(log)
+    stats["entries_applied"] += amount
+    stats["written"] = [v for _, v in log.entries[len(log.entries) - amount:]] if amount else []
     respond(dict(response, success=True, commit=message["leader-commit"],
                  **{"log-index": prev_index + len(message["entries"])}))
     n = candidate_to_follower(node)
@@ -387,6 +389,7 @@ class PyCluster:
         self.fault = {i: 0 for i in ids}
         self.trace = {i: FNV_OFFSET for i in ids}
         self.last_led = {i: 0 for i in ids}
+        self.stream = {i: [] for i in ids}
         self.hwm = (0, 0, 0)
         self.client_count = 0
         self.client_next = M32
@@ -490,7 +493,7 @@ class PyCluster:
                 sends.append((msg_src(msg), body))
 
             stats = {"entries_appended": 0, "entries_applied": 0, "appended_at": None,
-                     "elected": False, "match_changed": False}
+                     "elected": False, "match_changed": False, "written": []}
             cluster = self.cluster[i]
             try:
                 if msg is None:
@@ -521,6 +524,7 @@ class PyCluster:
             self.cnt[COUNTERS[ev - 1]] += 1
             self.cnt["entries_appended"] += stats["entries_appended"]
             self.cnt["entries_applied"] += stats["entries_applied"]
+            self.stream[i].extend(stats["written"])          # node_<id>.log (log.clj:16-18)
             if stats["appended_at"] is not None and len(log.entries) > stats["appended_at"]:
                 appended[i] = stats["appended_at"]
             if stats["elected"]:
@@ -616,7 +620,8 @@ class PyCluster:
                 "commit_index": log.commit_index & M32, "log_len": len(log.entries),
                 "deadline": self.deadline[i] & M32, "next_index": nxt, "match_index": mch,
                 "last_led_term": self.last_led[i], "trace_hash": self.trace[i],
-                "req_count": len(self.req[i]), "res_count": len(self.res[i])}
+                "req_count": len(self.req[i]), "res_count": len(self.res[i]),
+                "commit_count": len(self.stream[i]) & M32}
 
     def canonical_cluster(self):
         return {"hwm": tuple(self.hwm), "client_next": self.client_next,

@@ -71,6 +71,8 @@ struct raft_ref {
   raft_msg_t* q;        /* [C*N][2][Q], index 0 = head */
   raft_entry_t* arena;  /* [C*N][A] */
   raft_cluster_t* cl;   /* [C] */
+  uint32_t* stream;     /* [C*N][S] commit-stream rings (F2), S = commit_stream_cap */
+  uint32_t S;
   raft_counters_t ctr;
   int threads;
   uint64_t client_pw[32];
@@ -125,7 +127,9 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
   s->q = (raft_msg_t*)calloc(nn * 2 * s->Q, sizeof(raft_msg_t));
   s->arena = (raft_entry_t*)calloc(nn * s->A, sizeof(raft_entry_t));
   s->cl = (raft_cluster_t*)calloc(s->C, sizeof(raft_cluster_t));
-  if (!s->nodes || !s->q || !s->arena || !s->cl) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+  s->S = cfg->commit_stream_cap;
+  s->stream = (uint32_t*)calloc(nn * (s->S ? s->S : 1), sizeof(uint32_t));
+  if (!s->nodes || !s->q || !s->arena || !s->cl || !s->stream) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
   client_powers(cfg->client_ppm, s->client_pw);
   for (uint32_t c = 0; c < s->C; ++c) {
     uint32_t g = cfg->cluster_offset + c;
@@ -158,7 +162,7 @@ int raft_ref_set_threads(raft_ref_t* s, int threads) {
 
 void raft_ref_destroy(raft_ref_t* s) {
   if (!s) return;
-  free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s);
+  free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s->stream); free(s);
 }
 
 uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
@@ -174,7 +178,7 @@ typedef struct { int n; uint32_t arr[2]; raft_msg_t m; } cell_t;
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 typedef struct {
   int kind, reloc;
-  uint32_t old_base, old_len, src, poff, pcnt;
+  uint32_t old_base, old_len, src, poff, pcnt, applied;
   raft_entry_t entry;
 } plan_t;
 
@@ -449,6 +453,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
             uint32_t oldc = nn.commit_index;                        /* apply-entries! 69-76 */
             nn.commit_index = nn.log_len;
             applied = nn.commit_index > oldc ? nn.commit_index - oldc : 0;
+            plan[k].applied = (uint32_t)applied;
             r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 1, 0, 0);
             r.a = m.a; r.b = m.b + pcnt;
             nn.role = RAFT_FOLLWER; nn.voted_for = 0; nn.votes = 0; /* candidate->follower */
@@ -579,6 +584,19 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
           e = sa[(pl->poff + i) % s->A];
         ar[(dst + i) % s->A] = e;
       }
+    }
+  }
+
+  /* apply-entries! writes (F2): the :val's of the last `applied` entries (log.clj:69-76) */
+  for (uint32_t k = 0; k < N; ++k) {
+    uint32_t a = plan[k].applied;
+    if (!a) continue;
+    raft_node_t* n = &x->nodes[k];
+    const raft_entry_t* ar = arena_of(s, c * N + k);
+    uint32_t* ring = s->stream + (size_t)(c * N + k) * (s->S ? s->S : 1);
+    for (uint32_t i = n->log_len - a; i < n->log_len; ++i) {
+      if (s->S) ring[n->commit_count % s->S] = ar[(n->arena_base + i) % s->A].val;
+      n->commit_count++;
     }
   }
 
@@ -729,7 +747,7 @@ int raft_ref_write_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_nod
     uint32_t rq = d->req_count, rs = d->res_count;
     *d = in[i];
     d->req_count = rq; d->res_count = rs;
-    d->reserved0 = 0; d->reserved1 = 0;
+    d->reserved0 = 0;
     for (uint32_t p = N; p < RAFT_MAX_NODES; ++p) { d->next_index[p] = 0; d->match_index[p] = 0; }
   }
   return 0;
@@ -788,6 +806,29 @@ int raft_ref_write_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, const raf
   return 0;
 }
 
+int raft_ref_read_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t* out,
+                                uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  const raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
+  uint32_t kept = n->commit_count < s->S ? n->commit_count : s->S;
+  if (kept > cap) kept = cap;
+  const uint32_t* ring = s->stream + (size_t)(cluster * s->N + id - 1) * (s->S ? s->S : 1);
+  for (uint32_t i = 0; i < kept; ++i) out[i] = ring[(n->commit_count - kept + i) % s->S];
+  return (int)kept;
+}
+
+int raft_ref_write_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, const uint32_t* in,
+                                 uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  const raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
+  if (count > s->S || count > n->commit_count) return fail(-EINVAL, "count exceeds ring or commit_count");
+  uint32_t* ring = s->stream + (size_t)(cluster * s->N + id - 1) * (s->S ? s->S : 1);
+  for (uint32_t i = 0; i < count; ++i) ring[(n->commit_count - count + i) % s->S] = in[i];
+  return 0;
+}
+
 int raft_ref_read_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
@@ -829,6 +870,12 @@ int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
       h = fnv(h, (uint32_t)(n->trace_hash >> 32));
       h = fnv(h, n->arena_base);
       h = fnv(h, n->arena_frontier);
+      h = fnv(h, n->commit_count);
+      if (s->S) {
+        const uint32_t* ring = s->stream + (size_t)(c * N + k) * s->S;
+        uint32_t kept = n->commit_count < s->S ? n->commit_count : s->S;
+        for (uint32_t i = n->commit_count - kept; i != n->commit_count; ++i) h = fnv(h, ring[i % s->S]);
+      }
       for (int which = 0; which < 2; ++which) {
         uint32_t cnt = which ? n->res_count : n->req_count;
         h = fnv(h, cnt);

@@ -40,6 +40,10 @@ int raft_ref_read_arena(raft_ref_t* sim, uint32_t cluster, uint32_t node_id, raf
                         uint32_t cap);
 int raft_ref_write_arena(raft_ref_t* sim, uint32_t cluster, uint32_t node_id,
                          const raft_entry_t* in, uint32_t count);
+int raft_ref_read_commit_stream(raft_ref_t* sim, uint32_t cluster, uint32_t node_id,
+                                uint32_t* out, uint32_t cap);
+int raft_ref_write_commit_stream(raft_ref_t* sim, uint32_t cluster, uint32_t node_id,
+                                 const uint32_t* in, uint32_t count);
 int raft_ref_read_clusters(raft_ref_t* sim, uint32_t c0, uint32_t nc, raft_cluster_t* out);
 int raft_ref_write_clusters(raft_ref_t* sim, uint32_t c0, uint32_t nc, const raft_cluster_t* in);
 int raft_ref_read_counters(raft_ref_t* sim, raft_counters_t* out);

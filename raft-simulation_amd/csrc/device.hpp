@@ -34,6 +34,9 @@ struct DevSim {
   uint32_t* qbuf;         // [NN][2][Q][8]
   uint32_t* arena;        // [NN][A][2]
   uint32_t* cl;           // [C][8] raft_cluster_t
+  uint32_t* ccount;       // [NN] commit_count (F2)
+  uint32_t* stream;       // [NN][SC] commit-stream rings (F2)
+  uint32_t SC;            // commit_stream_cap
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)

@@ -126,6 +126,7 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   d.drop_ppm = cfg->drop_ppm; d.dup_ppm = cfg->dup_ppm; d.dmin = cfg->dmin; d.dmax = cfg->dmax;
   d.part_ppm = cfg->part_ppm; d.part_epoch = cfg->part_epoch; d.client_ppm = cfg->client_ppm;
   d.variant = cfg->variant_flags;
+  d.SC = cfg->commit_stream_cap;
   uint64_t pw[32];
   rs::client_powers(cfg->client_ppm, pw);
   d.client_pw = nullptr;
@@ -141,7 +142,9 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   if ((rc = dalloc(s, &d.next, NN * s->N)) || (rc = dalloc(s, &d.match, NN * s->N)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
       (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.cl, (size_t)s->C * 8)) ||
-      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1)) || (rc = dalloc(s, &s->client_pw, 32))) {
+      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1)) || (rc = dalloc(s, &s->client_pw, 32)) ||
+      (rc = dalloc(s, &d.ccount, NN)) ||
+      (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1)))) {
     raft_sim_destroy(s);
     return rc;
   }
@@ -155,6 +158,8 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.stream, 0, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1) * 4,
+                          s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
@@ -225,13 +230,13 @@ int raft_sim_read_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_node_t* ou
   if (!out) return fail(-EINVAL, "null output");
   HIP_OK(hipSetDevice(s->cfg.device));
   const size_t n0 = (size_t)c0 * s->N, cnt = (size_t)nc * s->N, NN = s->NN, N = s->N;
-  std::vector<uint32_t> w(16 * cnt);
+  std::vector<uint32_t> w(17 * cnt);
   std::vector<int32_t> nx(N * cnt), mt(N * cnt);
   const DevSim& d = s->d;
-  const uint32_t* src[16] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.qmeta,
+  const uint32_t* src[17] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.qmeta,
                              d.req_arr, d.res_arr, d.req_tail, d.res_tail, d.abase, d.afront,
-                             d.led, d.trace_lo, d.trace_hi};
-  for (int f = 0; f < 16; ++f) HIP_OK(d2h(s, &w[f * cnt], src[f] + n0, cnt));
+                             d.led, d.trace_lo, d.trace_hi, d.ccount};
+  for (int f = 0; f < 17; ++f) HIP_OK(d2h(s, &w[f * cnt], src[f] + n0, cnt));
   for (size_t p = 0; p < N; ++p) {
     HIP_OK(d2h(s, &nx[p * cnt], d.next + p * NN + n0, cnt));
     HIP_OK(d2h(s, &mt[p * cnt], d.match + p * NN + n0, cnt));
@@ -254,6 +259,7 @@ int raft_sim_read_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_node_t* ou
     r.arena_base = w[11 * cnt + i]; r.arena_frontier = w[12 * cnt + i];
     r.req_count = (qm >> 4) & 31; r.res_count = (qm >> 13) & 31;
     r.trace_hash = (uint64_t)w[15 * cnt + i] << 32 | w[14 * cnt + i];
+    r.commit_count = w[16 * cnt + i];
   }
   return 0;
 }
@@ -278,6 +284,7 @@ int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_nod
       return fail(-EINVAL, "invalid node record");
   }
   std::vector<uint32_t> w(14 * cnt);
+  std::vector<uint32_t> ccv(cnt);
   std::vector<int32_t> nx(N * cnt), mt(N * cnt);
   for (size_t i = 0; i < cnt; ++i) {
     const raft_node_t& r = in[i];
@@ -289,6 +296,7 @@ int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_nod
     w[6 * cnt + i] = r.arena_base; w[7 * cnt + i] = r.arena_frontier;
     w[8 * cnt + i] = r.last_led_term;
     w[9 * cnt + i] = (uint32_t)r.trace_hash; w[10 * cnt + i] = (uint32_t)(r.trace_hash >> 32);
+    ccv[i] = r.commit_count;
     for (size_t p = 0; p < N; ++p) {
       nx[p * cnt + i] = r.next_index[p];
       mt[p * cnt + i] = r.match_index[p];
@@ -298,6 +306,7 @@ int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_nod
   uint32_t* dst[11] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.abase,
                        d.afront, d.led, d.trace_lo, d.trace_hi};
   for (int f = 0; f < 11; ++f) HIP_OK(h2d(s, dst[f] + n0, &w[f * cnt], cnt));
+  HIP_OK(h2d(s, d.ccount + n0, ccv.data(), cnt));
   for (size_t p = 0; p < N; ++p) {
     HIP_OK(h2d(s, d.next + p * NN + n0, &nx[p * cnt], cnt));
     HIP_OK(h2d(s, d.match + p * NN + n0, &mt[p * cnt], cnt));
@@ -385,6 +394,45 @@ int raft_sim_write_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, const raf
   const size_t gi = (size_t)cluster * s->N + id - 1;
   HIP_OK(hipMemcpyAsync(s->d.arena + gi * s->A * 2, buf.data(), s->A * sizeof(raft_entry_t),
                         hipMemcpyHostToDevice, s->stream));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int raft_sim_read_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t* out,
+                                uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const uint32_t SC = s->cfg.commit_stream_cap;
+  const size_t gi = (size_t)cluster * s->N + id - 1;
+  uint32_t cc = 0;
+  std::vector<uint32_t> ring(std::max<uint32_t>(SC, 1));
+  HIP_OK(d2h(s, &cc, s->d.ccount + gi, 1));
+  if (SC) HIP_OK(d2h(s, ring.data(), s->d.stream + gi * SC, SC));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  uint32_t kept = std::min(std::min(cc, SC), cap);
+  for (uint32_t i = 0; i < kept && out; ++i) out[i] = ring[(cc - kept + i) % SC];
+  return (int)kept;
+}
+
+int raft_sim_write_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, const uint32_t* in,
+                                 uint32_t count) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  const uint32_t SC = s->cfg.commit_stream_cap;
+  const size_t gi = (size_t)cluster * s->N + id - 1;
+  uint32_t cc = 0;
+  HIP_OK(d2h(s, &cc, s->d.ccount + gi, 1));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  if (count > SC || count > cc || (count && !in))
+    return fail(-EINVAL, "count exceeds ring or commit_count");
+  if (!count) return 0;
+  std::vector<uint32_t> ring(SC);
+  HIP_OK(d2h(s, ring.data(), s->d.stream + gi * SC, SC));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  for (uint32_t i = 0; i < count; ++i) ring[(cc - count + i) % SC] = in[i];
+  HIP_OK(h2d(s, s->d.stream + gi * SC, ring.data(), SC));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }

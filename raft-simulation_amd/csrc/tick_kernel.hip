@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     const bool res_ok = live && n.rs.arr <= t;
     uint32_t sentmask = 0;
     uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, pold_len = 0,
-             preloc = 0, pet = 0, pev = 0;
+             preloc = 0, pet = 0, pev = 0, papplied = 0;
     int appended_at = -1;
     bool elected = false, mchg = false;
     if (live && (req_ok || res_ok || t >= n.deadline)) {
@@ -286,6 +286,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
               appended = pcnt;
               n.commit = n.len;                              // apply-entries! 69-76
               applied = n.commit > oldc ? n.commit - oldc : 0;
+              papplied = applied;
               n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;  // candidate->follower 75-78
               n.lid = src; n.term = mterm;
             }
@@ -365,6 +366,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
         lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
         pkind = PLAN_NONE;
+        papplied = 0;
         appended_at = -1;
         elected = false;
         mchg = false;
@@ -500,6 +502,15 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
           lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
         }
       }
+      if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
+        uint32_t cc = S.ccount[sgi];
+        uint32_t si = (n.base + n.len - papplied) % A;
+        for (uint32_t i = 0; i < papplied; ++i, ++cc) {
+          if (S.SC) S.stream[(size_t)sgi * S.SC + cc % S.SC] = sar[si].y;
+          si = si + 1 == A ? 0 : si + 1;
+        }
+        S.ccount[sgi] = cc;
+      }
     }
 
     // ---------------------------------------------------------------- P4 invariant checker
@@ -616,7 +627,7 @@ __global__ void init_kernel(DevSim S) {
   S.flags[gi] = 0; S.masks[gi] = 0; S.term[gi] = 1; S.commit[gi] = 0; S.len[gi] = 0;
   S.deadline[gi] = S.el_base + __umulhi(w.y, S.el_span);
   S.qmeta[gi] = 0; S.req_arr[gi] = INF; S.res_arr[gi] = INF; S.req_tail[gi] = 0;
-  S.res_tail[gi] = 0; S.abase[gi] = 0; S.afront[gi] = 0; S.led[gi] = 0;
+  S.res_tail[gi] = 0; S.abase[gi] = 0; S.afront[gi] = 0; S.led[gi] = 0; S.ccount[gi] = 0;
   S.trace_lo[gi] = 0x84222325u; S.trace_hi[gi] = 0xCBF29CE4u;
   if (id == 1) {                                   // cluster record: no hwm, first client-set
     uint32_t first = INF;
@@ -649,6 +660,12 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
     h = fnv(h, S.trace_hi[gi]);
     h = fnv(h, S.abase[gi]);
     h = fnv(h, S.afront[gi]);
+    const uint32_t cc = S.ccount[gi];
+    h = fnv(h, cc);
+    if (S.SC) {
+      const uint32_t kept = cc < S.SC ? cc : S.SC;
+      for (uint32_t i = cc - kept; i != cc; ++i) h = fnv(h, S.stream[(size_t)gi * S.SC + i % S.SC]);
+    }
     const uint32_t qh[2] = {qm & 15, (qm >> 9) & 15}, qc[2] = {(qm >> 4) & 31, (qm >> 13) & 31};
     for (int which = 0; which < 2; ++which) {
       h = fnv(h, qc[which]);

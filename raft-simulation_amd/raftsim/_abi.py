@@ -26,7 +26,7 @@ class Config(C.Structure):
                 ("part_ppm", C.c_uint32), ("part_epoch", C.c_uint32),
                 ("client_ppm", C.c_uint32), ("variant_flags", C.c_uint32),
                 ("device", C.c_int32), ("ticks_per_launch", C.c_uint32),
-                ("reserved", C.c_uint32 * 4)]
+                ("commit_stream_cap", C.c_uint32), ("reserved", C.c_uint32 * 3)]
 
 
 class Node(C.Structure):
@@ -38,7 +38,7 @@ class Node(C.Structure):
                 ("next_index", C.c_int32 * MAX_NODES), ("match_index", C.c_int32 * MAX_NODES),
                 ("last_led_term", C.c_uint32), ("arena_base", C.c_uint32),
                 ("arena_frontier", C.c_uint32), ("req_count", C.c_uint32),
-                ("res_count", C.c_uint32), ("reserved1", C.c_uint32),
+                ("res_count", C.c_uint32), ("commit_count", C.c_uint32),
                 ("trace_hash", C.c_uint64)]
 
     def as_dict(self, n_nodes):
@@ -98,6 +98,10 @@ _SIGS = {
                               C.c_uint32]),
     "read_arena": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Entry), C.c_uint32]),
     "write_arena": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Entry), C.c_uint32]),
+    "read_commit_stream": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32),
+                                     C.c_uint32]),
+    "write_commit_stream": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32),
+                                      C.c_uint32]),
     "read_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
     "write_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
     "read_counters": (C.c_int, [C.c_void_p, P(Counters)]),

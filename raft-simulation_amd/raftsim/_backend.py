@@ -133,6 +133,27 @@ class Backend:
         A = len(ar)
         return [ar[(rec["arena_base"] + i) % A] for i in range(rec["log_len"])]
 
+    def commit_stream(self, cluster, node_id):
+        """F2: the committed :val's apply-entries! wrote to node_<id>.log (log.clj:69-76), as far
+        back as the configured ring (commit_stream_cap) reaches, oldest first."""
+        cap = max(1, self.config.commit_stream_cap)
+        buf = (C.c_uint32 * cap)()
+        n = self._check(self._fns["read_commit_stream"](self._h, cluster, node_id, buf, cap))
+        return list(buf[:n])
+
+    def write_commit_stream(self, cluster, node_id, vals):
+        buf = (C.c_uint32 * max(1, len(vals)))(*vals)
+        self._check(self._fns["write_commit_stream"](self._h, cluster, node_id, buf, len(vals)))
+
+    def write_commit_logs(self, directory, cluster=0):
+        """Write node_<id>.log files the way the reference's Log component does (log.clj:16-18):
+        one committed value per line. Only the retained tail of the stream is available."""
+        from pathlib import Path
+        d = Path(directory)
+        d.mkdir(parents=True, exist_ok=True)
+        for i in range(1, self.N + 1):
+            (d / f"node_{i}.log").write_text("".join(f"{v}\n" for v in self.commit_stream(cluster, i)))
+
     def read_clusters(self, c0=0, nc=None):
         """Per-cluster records: checker high-water mark and client-injection cursor."""
         nc = self.C - c0 if nc is None else nc

@@ -24,7 +24,7 @@ def py_config(**cfg):
 NODE_FIELDS = ["role", "voted_for", "leader_id", "fault", "entries_is_seq", "ls_present",
                "votes", "ls_keys", "current_term", "commit_index", "log_len", "deadline",
                "next_index", "match_index", "last_led_term", "trace_hash", "req_count",
-               "res_count"]
+               "res_count", "commit_count"]
 
 
 def compare_py_backend(pc: "pyref.PyCluster", be: Backend, cluster: int):
@@ -37,6 +37,10 @@ def compare_py_backend(pc: "pyref.PyCluster", be: Backend, cluster: int):
             assert got[f] == want[f], (f"node {i} field {f}: backend {got[f]} != py {want[f]}",
                                        got, want)
         assert be.log(cluster, i) == [tuple(e) for e in pc.logs[i].entries], f"node {i} log"
+        cap = be.config.commit_stream_cap
+        if cap:
+            want_s = pc.stream[i][len(pc.stream[i]) - min(cap, len(pc.stream[i])):]
+            assert be.commit_stream(cluster, i) == want_s, f"node {i} commit stream"
         for which in (0, 1):
             gq = be.read_queue(cluster, i, which)
             wq = pc.canonical_msgs(i, which)

@@ -30,7 +30,7 @@ class Scenario:
     def __init__(self, N, nodes, queues=None, hwm=(0, 0, 0), **cfg):
         self.N, self.nodes, self.hwm = N, nodes, hwm
         self.queues = queues or {}
-        self.cfg = dict(dict(nodes=N, n_clusters=1, log_cap=64), **cfg)
+        self.cfg = dict(dict(nodes=N, n_clusters=1, log_cap=64, commit_stream_cap=64), **cfg)
 
     # ---------------------------------------------------------------- C ABI backends
     def load_backend(self, make):
@@ -134,6 +134,9 @@ class PyView:
     def counters(self):
         return dict(self.pc.cnt)
 
+    def commit_stream(self, i):
+        return list(self.pc.stream[i])
+
 
 class BackendView:
     def __init__(self, be):
@@ -150,6 +153,9 @@ class BackendView:
 
     def counters(self):
         return self.be.counters()
+
+    def commit_stream(self, i):
+        return self.be.commit_stream(0, i)
 
 
 def run(scn, which, make=None):
@@ -238,6 +244,8 @@ def kat_duplication(view_of):
     assert v.log(2) == [E2, E3, E3] and v.log(3) == [E2, E3, E3]
     v.step(3003)
     assert v.log(2) == [E2, E3, E3, E3]         # one more e3 per heartbeat
+    # node_2.log (log.clj:16-18,69-76): each apply writes the take-last `amount` :val's
+    assert v.commit_stream(2) == [20, 30, 30, 30]
     assert v.counters()["viol_log"] >= 1        # same index and term, different value
 
 

@@ -44,5 +44,8 @@ class _Both:
     def log(self, i):
         return self.a.log(i)
 
+    def commit_stream(self, i):
+        return self.a.commit_stream(i)
+
     def counters(self):
         return self.a.counters()

@@ -19,12 +19,13 @@ CASES = {
     # C3 shape: faults, partitions, client-set
     "c3_faults": dict(n_clusters=2048, nodes=5, seed=1, client_ppm=1000, log_cap=256, **FAULTS),
     # C4 shape: 7 and 9 nodes, client-heavy, long logs
-    "c4_n7": dict(n_clusters=1024, nodes=7, seed=3, client_ppm=3000, log_cap=512),
+    "c4_n7": dict(n_clusters=1024, nodes=7, seed=3, client_ppm=3000, log_cap=512,
+                  commit_stream_cap=256),
     "c4_n9": dict(n_clusters=512, nodes=9, seed=5, client_ppm=2000, log_cap=1024, dup_ppm=20000,
                   dmax=8),
     # C5: bug variant (vote granted without the log check)
     "c5_variant": dict(n_clusters=1024, nodes=5, seed=9, client_ppm=1000, log_cap=256,
-                       variant_flags=1, **FAULTS),
+                       variant_flags=1, commit_stream_cap=7, **FAULTS),
     # overflow and tiny inboxes, heavy duplication
     "overflow": dict(n_clusters=512, nodes=9, seed=11, inbox_cap=2, dup_ppm=300000, dmax=3,
                      client_ppm=5000, log_cap=64),

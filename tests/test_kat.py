@@ -47,5 +47,8 @@ class _Both:
     def log(self, i):
         return self.py.log(i)
 
+    def commit_stream(self, i):
+        return self.py.commit_stream(i)
+
     def counters(self):
         return self.py.counters()

@@ -43,6 +43,7 @@ def random_config(rng):
         cfg["variant_flags"] = 1
     if rng.random() < 0.3:
         cfg["arena_cap"] = 2 * cfg["log_cap"]
+    cfg["commit_stream_cap"] = rng.choice([0, 3, 64])
     return cfg
 
 
@@ -76,6 +77,19 @@ def test_message_conservation():
     c = be.counters()
     assert (c["sent"] + c["client_injected"] - c["dropped"] - c["partitioned"] + c["duplicated"]
             == c["delivered"] + c["overflow"] + c["to_halted"])
+
+
+def test_commit_logs_written_like_the_reference(tmp_path):
+    """F2: node_<id>.log holds one committed :val per line (log.clj:16-18)."""
+    be = helpers.oracle(n_clusters=4, nodes=5, seed=7, client_ppm=3000, log_cap=256,
+                        commit_stream_cap=4096)
+    be.step(30000)
+    be.write_commit_logs(tmp_path, cluster=2)
+    for i in range(1, 6):
+        lines = (tmp_path / f"node_{i}.log").read_text().splitlines()
+        assert [int(x) for x in lines] == be.commit_stream(2, i)
+        assert len(lines) == be.read_nodes(2, 1)[i - 1]["commit_count"]
+    assert be.counters()["entries_applied"] == sum(r["commit_count"] for r in be.read_nodes())
 
 
 def test_threads_do_not_change_results():
