@@ -63,7 +63,9 @@ typedef struct raft_sim_config {
   int32_t device;            /* HIP device ordinal */
   uint32_t ticks_per_launch; /* ticks fused into one kernel launch; 0 -> default */
   uint32_t commit_stream_cap; /* per-node ring of committed :val's (log.clj:69-76); 0 = off */
-  uint32_t reserved[3];
+  uint32_t trace_cap;         /* per-node ring of `wait` events (core.clj:182-186); 0 = off */
+  uint32_t trace_entry_cap;   /* per-node ring of the :entries those events carried */
+  uint32_t reserved[1];
 } raft_sim_config_t;
 
 /* Canonical node record: the node map of init-node (core.clj:31-38) plus the log atom
@@ -100,6 +102,22 @@ typedef struct raft_cluster {
   uint32_t client_next, client_count;
   uint32_t reserved[3];
 } raft_cluster_t;
+
+/* F3: one iteration of `wait` as it prints (core.clj:182-186): the node map before the handler
+ * (`; Node` / `(prn node)`) and the message alts!! returned (`; Message` / `(prn message)`). A
+ * timeout (`nil`) has an all-zero msg. An append-entries' :entries are the msg.hdr>>16 entries of
+ * the node's trace-entry ring starting at entries_seq (SIM_SPEC §7). */
+typedef struct raft_trace_event {
+  uint32_t tick;
+  uint32_t seq;            /* this node's event number, from 0 */
+  raft_msg_t msg;          /* as queued: arrival, hdr, term, a, b, eterm, eval, poff */
+  uint8_t role, voted_for, leader_id, ls_present;
+  uint16_t votes, ls_keys;
+  uint32_t current_term;
+  int32_t next_index[RAFT_MAX_NODES];
+  int32_t match_index[RAFT_MAX_NODES];
+  uint32_t entries_seq;
+} raft_trace_event_t;
 
 enum raft_counter {
   RAFT_CTR_EV_RV = 0, RAFT_CTR_EV_AE, RAFT_CTR_EV_CS, RAFT_CTR_EV_VR, RAFT_CTR_EV_AR,
@@ -157,6 +175,15 @@ int raft_sim_read_commit_stream(raft_sim_t* sim, uint32_t cluster, uint32_t node
                                 uint32_t* out, uint32_t cap);
 int raft_sim_write_commit_stream(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
                                  const uint32_t* in, uint32_t count);
+
+/* F3: the retained events of node `node_id` with seq >= first_seq, oldest first (the newest
+ * trace_cap are kept); returns how many were copied. read_trace_entries copies the entries with
+ * ring index first, first+1, ... (at most cap, up to the newest) and returns how many; -ERANGE if
+ * entry `first` has already been overwritten (only the newest trace_entry_cap are kept). */
+int raft_sim_read_trace(raft_sim_t* sim, uint32_t cluster, uint32_t node_id, uint32_t first_seq,
+                        raft_trace_event_t* out, uint32_t cap);
+int raft_sim_read_trace_entries(raft_sim_t* sim, uint32_t cluster, uint32_t node_id,
+                                uint32_t first, raft_entry_t* out, uint32_t cap);
 
 int raft_sim_read_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_cluster_t* out);
 int raft_sim_write_clusters(raft_sim_t* sim, uint32_t c0, uint32_t nc, const raft_cluster_t* in);

@@ -16,6 +16,8 @@ agreement with the independently written C oracle (tests/test_oracle.py, tests/t
 """
 from __future__ import annotations
 
+import copy
+
 M32 = 0xFFFFFFFF
 
 # ----------------------------------------------------------------------------------------------
@@ -356,7 +358,7 @@ COUNTERS = ["ev_rv", "ev_ae", "ev_cs", "ev_vr", "ev_ar", "ev_timeout", "ev_heart
 def default_config(**kw):
     cfg = dict(nodes=5, log_cap=64, arena_cap=0, inbox_cap=16, seed=42, hb=3000, el_base=5000,
                el_span=5000, drop_ppm=0, dup_ppm=0, dmin=1, dmax=1, part_ppm=0, part_epoch=1000,
-               client_ppm=0, variant_flags=0)
+               client_ppm=0, variant_flags=0, trace_cap=0)
     cfg.update(kw)
     return cfg
 
@@ -390,6 +392,7 @@ class PyCluster:
         self.trace = {i: FNV_OFFSET for i in ids}
         self.last_led = {i: 0 for i in ids}
         self.stream = {i: [] for i in ids}
+        self.events = {i: [] for i in ids}   # (tick, node before the handler, message) per wait
         self.hwm = (0, 0, 0)
         self.client_count = 0
         self.client_next = M32
@@ -484,6 +487,8 @@ class PyCluster:
                 q = None
             node, log = self.nodes[i], self.logs[i]
             msg = q.pop(0)[1] if q is not None else None
+            if cfg.get("trace_cap"):                         # (prn node) (prn message), 182-186
+                self.events[i].append((t, copy.deepcopy(node), copy.deepcopy(msg)))
             sends = []
 
             def rpc(p, m, sends=sends):
@@ -668,6 +673,67 @@ def encode_msg(arrival, m):
         epresent, eterm, evalue = 1, e[0], e[1]
     hdr = code | src << 3 | flag << 7 | epresent << 8 | len(payload) << 16
     return (arrival & M32, hdr, term & M32, a & M32, b & M32, eterm & M32, evalue & M32, payload)
+
+
+# ----------------------------------------------------------------------------------------------
+# prn (core.clj:182-186) of the values above, restated for the F3 trace cross-check
+# ----------------------------------------------------------------------------------------------
+def prn(v, chan=None):
+    """Clojure's printed form of a node map / message held in this module's shapes: dict keys
+    and `type` values become keywords, (term, val) entries become {:term t, :val v}. Integer-keyed
+    maps and sets print in ascending key order (see SIM_SPEC §7)."""
+    if v is None:
+        return "nil"
+    if v is True or v is False:
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, str):
+        return v if v.startswith(":") or v.startswith("#<") else ":" + v
+    if isinstance(v, tuple):
+        return "{:term %d, :val %d}" % v
+    if isinstance(v, set):
+        return "#{" + " ".join(str(x) for x in sorted(v)) + "}"
+    if isinstance(v, list):
+        return "[" + " ".join(prn(x) for x in v) + "]"
+    keys = sorted(v) if all(isinstance(k, int) for k in v) else list(v)
+    return "{" + ", ".join(f"{prn(k) if isinstance(k, int) else ':' + k} {prn(v[k])}"
+                           for k in keys) + "}"
+
+
+def printed_message(msg, seq):
+    """The message as the receiving `wait` holds it: a request is its JSON body in the sender's
+    key order plus :type (server.clj:14-16) and :resp-chan (server.clj:21); a reply is the body."""
+    if msg is None:
+        return None
+    order = BODY_ORDER[msg["type"]]
+    m = {k: msg[k] for k in order if k in msg}
+    if TYPE_CODE[msg["type"]] in REQ_TYPES:
+        m["type"] = msg["type"]
+        m["resp-chan"] = ("#<ManyToManyChannel clojure.core.async.impl.channels."
+                          "ManyToManyChannel@%x>" % seq)
+    return m
+
+
+BODY_ORDER = {   # literal key order of each body: core.clj:51-54, 62-67, 94+98/100, 108+110-121
+    "request-vote": ["term", "candidate-id", "last-log-index", "last-log-term"],
+    "append-entries": ["term", "leader-id", "leader-commit", "prev-log-index", "prev-log-term",
+                       "entries"],
+    "client-set": ["command"],
+    "vote-response": ["term", "id", "type", "vote-granted"],
+    "append-response": ["term", "id", "type", "success", "commit", "log-index"],
+}
+
+
+def stdout_of(cluster, i, first=0):
+    """What node i's JVM prints over the recorded events from event `first` on."""
+    out = []
+    for seq, (_, node, msg) in enumerate(cluster.events[i]):
+        if seq < first:
+            continue
+        out.append("; Node\n" + prn(node) + "\n; Message\n" + prn(printed_message(msg, seq))
+                   + "\n\n")
+    return "".join(out)
 
 
 def run(cfg, gid, ticks, t0=0):

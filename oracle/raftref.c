@@ -73,6 +73,11 @@ struct raft_ref {
   raft_cluster_t* cl;   /* [C] */
   uint32_t* stream;     /* [C*N][S] commit-stream rings (F2), S = commit_stream_cap */
   uint32_t S;
+  raft_trace_event_t* tr; /* [C*N][TC] wait-event rings (F3) */
+  uint32_t* tcount;       /* [C*N] events recorded per node */
+  raft_entry_t* tent;     /* [C*N][TE] :entries carried by recorded append-entries */
+  uint32_t* tecount;      /* [C*N] */
+  uint32_t TC, TE;
   raft_counters_t ctr;
   int threads;
   uint64_t client_pw[32];
@@ -108,6 +113,8 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->part_epoch < 1) return fail(-EINVAL, "part_epoch must be >= 1");
   if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
       c->client_ppm > 1000000) return fail(-EINVAL, "ppm values must be <= 1e6");
+  if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
+    return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
   return 0;
 }
 
@@ -129,7 +136,13 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
   s->cl = (raft_cluster_t*)calloc(s->C, sizeof(raft_cluster_t));
   s->S = cfg->commit_stream_cap;
   s->stream = (uint32_t*)calloc(nn * (s->S ? s->S : 1), sizeof(uint32_t));
-  if (!s->nodes || !s->q || !s->arena || !s->cl || !s->stream) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+  s->TC = cfg->trace_cap; s->TE = cfg->trace_entry_cap;
+  s->tr = (raft_trace_event_t*)calloc(nn * (s->TC ? s->TC : 1), sizeof(raft_trace_event_t));
+  s->tcount = (uint32_t*)calloc(nn, sizeof(uint32_t));
+  s->tent = (raft_entry_t*)calloc(nn * (s->TE ? s->TE : 1), sizeof(raft_entry_t));
+  s->tecount = (uint32_t*)calloc(nn, sizeof(uint32_t));
+  if (!s->nodes || !s->q || !s->arena || !s->cl || !s->stream || !s->tr || !s->tcount || !s->tent ||
+      !s->tecount) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
   client_powers(cfg->client_ppm, s->client_pw);
   for (uint32_t c = 0; c < s->C; ++c) {
     uint32_t g = cfg->cluster_offset + c;
@@ -162,7 +175,8 @@ int raft_ref_set_threads(raft_ref_t* s, int threads) {
 
 void raft_ref_destroy(raft_ref_t* s) {
   if (!s) return;
-  free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s->stream); free(s);
+  free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s->stream);
+  free(s->tr); free(s->tcount); free(s->tent); free(s->tecount); free(s);
 }
 
 uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
@@ -359,6 +373,10 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
 
   plan_t plan[RAFT_MAX_NODES];
   int appended_at[RAFT_MAX_NODES];
+  /* F3: append-entries whose :entries the trace records (src, poff, count, ring index) */
+  uint32_t tr_src[RAFT_MAX_NODES], tr_poff[RAFT_MAX_NODES], tr_cnt[RAFT_MAX_NODES];
+  uint32_t tr_at[RAFT_MAX_NODES];
+  memset(tr_cnt, 0, sizeof tr_cnt);
   uint32_t elected = 0, match_changed = 0;
   const uint32_t h_index = cr->hwm_index, h_term = cr->hwm_term, h_val = cr->hwm_val;
   memset(plan, 0, sizeof plan);
@@ -387,6 +405,24 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
       memmove(q, q + 1, (*cnt - 1) * sizeof *q);
       (*cnt)--;
       memset(&q[*cnt], 0, sizeof *q);
+    }
+    if (s->TC) {               /* `; Node` (prn node) `; Message` (prn message), core.clj:182-186 */
+      uint32_t* tc = &s->tcount[gi];
+      raft_trace_event_t* ev = &s->tr[(size_t)gi * s->TC + *tc % s->TC];
+      memset(ev, 0, sizeof *ev);
+      ev->tick = t; ev->seq = *tc; ev->msg = m;
+      ev->role = n->role; ev->voted_for = n->voted_for; ev->leader_id = n->leader_id;
+      ev->ls_present = n->ls_present; ev->votes = n->votes; ev->ls_keys = n->ls_keys;
+      ev->current_term = n->current_term;
+      memcpy(ev->next_index, n->next_index, sizeof ev->next_index);
+      memcpy(ev->match_index, n->match_index, sizeof ev->match_index);
+      ev->entries_seq = s->tecount[gi];
+      if ((m.hdr & 7) == RAFT_MSG_APPEND_ENTRIES && which >= 0) {
+        tr_src[k] = (m.hdr >> 3) & 15; tr_poff[k] = m.poff; tr_cnt[k] = m.hdr >> 16;
+        tr_at[k] = s->tecount[gi];
+        s->tecount[gi] += tr_cnt[k];
+      }
+      (*tc)++;
     }
     raft_node_t nn = *n;
     emit_t em[RAFT_MAX_NODES];
@@ -584,6 +620,20 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
           e = sa[(pl->poff + i) % s->A];
         ar[(dst + i) % s->A] = e;
       }
+    }
+  }
+
+  /* F3: the :entries of traced append-entries, as P3 resolves them (evicted -> (0,0)) */
+  for (uint32_t k = 0; k < N && s->TE; ++k) {
+    if (!tr_cnt[k]) continue;
+    const raft_node_t* sn = &x->nodes[tr_src[k] - 1];
+    const raft_entry_t* sa = arena_of(s, c * N + tr_src[k] - 1);
+    raft_entry_t* ring = s->tent + (size_t)(c * N + k) * s->TE;
+    for (uint32_t i = 0; i < tr_cnt[k]; ++i) {
+      raft_entry_t e = {0, 0};
+      if ((uint64_t)sn->arena_frontier <= (uint64_t)tr_poff[k] + i + s->A)
+        e = sa[(tr_poff[k] + i) % s->A];
+      ring[(tr_at[k] + i) % s->TE] = e;
     }
   }
 
@@ -829,6 +879,32 @@ int raft_ref_write_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, c
   return 0;
 }
 
+int raft_ref_read_trace(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+                        raft_trace_event_t* out, uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  uint32_t gi = cluster * s->N + id - 1, cnt = s->tcount[gi];
+  uint32_t lo = cnt > s->TC ? cnt - s->TC : 0;
+  if (first > lo) lo = first;
+  uint32_t n = 0;
+  for (uint32_t i = lo; i < cnt && n < cap; ++i) out[n++] = s->tr[(size_t)gi * s->TC + i % s->TC];
+  return (int)n;
+}
+
+int raft_ref_read_trace_entries(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+                                raft_entry_t* out, uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  if (!s->TE) return fail(-ERANGE, "trace_entry_cap is 0");
+  uint32_t gi = cluster * s->N + id - 1, cnt = s->tecount[gi];
+  uint32_t lo = cnt > s->TE ? cnt - s->TE : 0;
+  if (first < lo) return fail(-ERANGE, "trace entries overwritten (ring holds the newest)");
+  lo = first;
+  uint32_t n = 0;
+  for (uint32_t i = lo; i < cnt && n < cap; ++i) out[n++] = s->tent[(size_t)gi * s->TE + i % s->TE];
+  return (int)n;
+}
+
 int raft_ref_read_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
@@ -875,6 +951,23 @@ int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
         const uint32_t* ring = s->stream + (size_t)(c * N + k) * s->S;
         uint32_t kept = n->commit_count < s->S ? n->commit_count : s->S;
         for (uint32_t i = n->commit_count - kept; i != n->commit_count; ++i) h = fnv(h, ring[i % s->S]);
+      }
+      if (s->TC) {                /* F3 trace rings, retained part, oldest first */
+        uint32_t gi = c * N + k, cnt = s->tcount[gi], kept = cnt < s->TC ? cnt : s->TC;
+        h = fnv(h, cnt);
+        for (uint32_t i = cnt - kept; i != cnt; ++i) {
+          const uint32_t* wds = (const uint32_t*)&s->tr[(size_t)gi * s->TC + i % s->TC];
+          for (int j = 0; j < 32; ++j) h = fnv(h, wds[j]);
+        }
+      }
+      if (s->TE) {
+        uint32_t gi = c * N + k, cnt = s->tecount[gi], kept = cnt < s->TE ? cnt : s->TE;
+        h = fnv(h, cnt);
+        for (uint32_t i = cnt - kept; i != cnt; ++i) {
+          raft_entry_t e = s->tent[(size_t)gi * s->TE + i % s->TE];
+          h = fnv(h, e.term);
+          h = fnv(h, e.val);
+        }
       }
       for (int which = 0; which < 2; ++which) {
         uint32_t cnt = which ? n->res_count : n->req_count;

@@ -44,6 +44,10 @@ int raft_ref_read_commit_stream(raft_ref_t* sim, uint32_t cluster, uint32_t node
                                 uint32_t* out, uint32_t cap);
 int raft_ref_write_commit_stream(raft_ref_t* sim, uint32_t cluster, uint32_t node_id,
                                  const uint32_t* in, uint32_t count);
+int raft_ref_read_trace(raft_ref_t* sim, uint32_t cluster, uint32_t node_id, uint32_t first_seq,
+                        raft_trace_event_t* out, uint32_t cap);
+int raft_ref_read_trace_entries(raft_ref_t* sim, uint32_t cluster, uint32_t node_id,
+                                uint32_t first, raft_entry_t* out, uint32_t cap);
 int raft_ref_read_clusters(raft_ref_t* sim, uint32_t c0, uint32_t nc, raft_cluster_t* out);
 int raft_ref_write_clusters(raft_ref_t* sim, uint32_t c0, uint32_t nc, const raft_cluster_t* in);
 int raft_ref_read_counters(raft_ref_t* sim, raft_counters_t* out);

@@ -37,6 +37,11 @@ struct DevSim {
   uint32_t* ccount;       // [NN] commit_count (F2)
   uint32_t* stream;       // [NN][SC] commit-stream rings (F2)
   uint32_t SC;            // commit_stream_cap
+  uint32_t* tr;           // [NN][TC][32] wait-event records (F3, raft_trace_event_t)
+  uint32_t* tcount;       // [NN]
+  uint2* tent;            // [NN][TE] :entries of recorded append-entries
+  uint32_t* tecount;      // [NN]
+  uint32_t TC, TE;
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)

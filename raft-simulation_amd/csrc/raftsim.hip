@@ -73,6 +73,8 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
       c->client_ppm > 1000000)
     return fail(-EINVAL, "ppm values must be <= 1e6");
+  if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
+    return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
   return 0;
 }
 
@@ -127,6 +129,8 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   d.part_ppm = cfg->part_ppm; d.part_epoch = cfg->part_epoch; d.client_ppm = cfg->client_ppm;
   d.variant = cfg->variant_flags;
   d.SC = cfg->commit_stream_cap;
+  d.TC = cfg->trace_cap;
+  d.TE = cfg->trace_entry_cap;
   uint64_t pw[32];
   rs::client_powers(cfg->client_ppm, pw);
   d.client_pw = nullptr;
@@ -144,7 +148,11 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.cl, (size_t)s->C * 8)) ||
       (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1)) || (rc = dalloc(s, &s->client_pw, 32)) ||
       (rc = dalloc(s, &d.ccount, NN)) ||
-      (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1)))) {
+      (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1))) ||
+      (rc = dalloc(s, &d.tr, NN * std::max<uint32_t>(d.TC, 1) * 32)) ||
+      (rc = dalloc(s, &d.tcount, NN)) ||
+      (rc = dalloc(s, &d.tent, NN * std::max<uint32_t>(d.TE, 1))) ||
+      (rc = dalloc(s, &d.tecount, NN))) {
     raft_sim_destroy(s);
     return rc;
   }
@@ -160,6 +168,10 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.stream, 0, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1) * 4,
                           s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.tr, 0, NN * std::max<uint32_t>(d.TC, 1) * 128, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.tcount, 0, NN * 4, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.tent, 0, NN * std::max<uint32_t>(d.TE, 1) * 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.tecount, 0, NN * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
@@ -435,6 +447,50 @@ int raft_sim_write_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, c
   HIP_OK(h2d(s, s->d.stream + gi * SC, ring.data(), SC));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
+}
+
+// F3 rings: copy the retained items with index >= first (oldest first), at most cap of them;
+// `strict` rejects a `first` that has been overwritten instead of starting at the oldest kept.
+template <typename T>
+static int read_ring(raft_sim* s, const uint32_t* dcount, const T* dring, uint32_t R, uint32_t gi,
+                     uint32_t first, T* out, uint32_t cap, bool strict) {
+  uint32_t cnt = 0;
+  HIP_OK(d2h(s, &cnt, dcount + gi, 1));
+  HIP_OK(hipStreamSynchronize(s->stream));
+  uint32_t lo = cnt > R ? cnt - R : 0;
+  if (strict && first < lo) return fail(-ERANGE, "trace entries overwritten (ring holds the newest)");
+  if (first > lo) lo = first;
+  const uint32_t n = lo < cnt ? std::min(cnt - lo, cap) : 0;
+  if (n && !out) return fail(-EINVAL, "null output");
+  // at most two contiguous pieces of the ring
+  for (uint32_t done = 0; done < n;) {
+    const uint32_t slot = (lo + done) % R, run = std::min(n - done, R - slot);
+    HIP_OK(d2h(s, out + done, dring + (size_t)gi * R + slot, run));
+    done += run;
+  }
+  HIP_OK(hipStreamSynchronize(s->stream));
+  return (int)n;
+}
+
+int raft_sim_read_trace(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+                        raft_trace_event_t* out, uint32_t cap) {
+  static_assert(sizeof(raft_trace_event_t) == 128, "trace record is 32 words");
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  if (!s->d.TC) return 0;
+  return read_ring(s, s->d.tcount, reinterpret_cast<const raft_trace_event_t*>(s->d.tr),
+                   s->d.TC, cluster * s->N + id - 1, first, out, cap, false);
+}
+
+int raft_sim_read_trace_entries(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+                                raft_entry_t* out, uint32_t cap) {
+  int rc = check_node(s, cluster, id);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(s->cfg.device));
+  if (!s->d.TE) return fail(-ERANGE, "trace_entry_cap is 0");
+  return read_ring(s, s->d.tecount, reinterpret_cast<const raft_entry_t*>(s->d.tent), s->d.TE,
+                   cluster * s->N + id - 1, first, out, cap, true);
 }
 
 int raft_sim_read_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {

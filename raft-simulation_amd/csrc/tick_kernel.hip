@@ -59,7 +59,32 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
+// F3: record one `wait` iteration (core.clj:182-186) — the node map before the handler and the
+// message alts!! returned — as a raft_trace_event_t (32 words) in the node's ring.
 template <int N>
+__device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint32_t t,
+                                             const NodeR& n, uint4 m0, uint4 m1, uint32_t tes) {
+  const uint32_t seq = S.tcount[gi];
+  S.tcount[gi] = seq + 1;
+  uint32_t w[32];
+  w[0] = t; w[1] = seq;
+  w[2] = m0.x; w[3] = m0.y; w[4] = m0.z; w[5] = m0.w;
+  w[6] = m1.x; w[7] = m1.y; w[8] = m1.z; w[9] = m1.w;
+  w[10] = n.role | n.vf << 8 | n.lid << 16 | n.lsp << 24;
+  w[11] = n.votes | n.keys << 16;
+  w[12] = n.term;
+#pragma unroll
+  for (int p = 0; p < RAFT_MAX_NODES; ++p) {
+    w[13 + p] = p < N ? (uint32_t)S.next[p * S.NN + gi] : 0u;
+    w[22 + p] = p < N ? (uint32_t)S.match[p * S.NN + gi] : 0u;
+  }
+  w[31] = tes;
+  uint4* rec = reinterpret_cast<uint4*>(S.tr + ((size_t)gi * S.TC + seq % S.TC) * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+template <int N, bool TRACE>
 __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr int CELL_WORDS = CPW * N * N * 8;
@@ -157,6 +182,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
              preloc = 0, pet = 0, pev = 0, papplied = 0;
     int appended_at = -1;
     bool elected = false, mchg = false;
+    uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
     if (live && (req_ok || res_ok || t >= n.deadline)) {
       // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
       // and for the next timeout of a non-leader (core.clj:174); leaders' events skip it.
@@ -192,6 +218,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
                      mpoff = m1.w;
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
                      mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
+      if constexpr (TRACE) {
+        const uint32_t tes = S.tecount[sgi];
+        trace_record<N>(S, sgi, t, n, m0, m1, tes);
+        if (which >= 0 && type == RAFT_MSG_APPEND_ENTRIES && pcnt) {
+          tr_cnt = pcnt; tr_src = src; tr_poff = mpoff; tr_at = tes;
+          S.tecount[sgi] = tes + pcnt;
+        }
+      }
 
       // Every throw site of the reference precedes every mutation of its handler (SIM_SPEC D8),
       // so each case decides `fault` first and only then updates the node in place.
@@ -468,7 +502,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     }
 
     // ---------------------------------------------------------------- P3 log writes
-    if (__ballot(pkind != PLAN_NONE)) {
+    if (__ballot(pkind != PLAN_NONE || (TRACE && tr_cnt))) {
       const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
       if (pkind != PLAN_NONE && m) {
@@ -510,6 +544,18 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
           si = si + 1 == A ? 0 : si + 1;
         }
         S.ccount[sgi] = cc;
+      }
+      if constexpr (TRACE) {   // the traced message's :entries, resolved like the payload above
+        const uint32_t tfront = __shfl(n.front, bl + (int)tr_src - 1);
+        if (tr_cnt && S.TE) {
+          const int64_t ev = (int64_t)tfront - (int64_t)A - (int64_t)tr_poff;
+          const uint32_t evicted = ev <= 0 ? 0u : (ev >= (int64_t)tr_cnt ? tr_cnt : (uint32_t)ev);
+          const uint2* sa = arena_of(S, sgi - k + tr_src - 1);
+          uint2* ring = S.tent + (size_t)sgi * S.TE;
+          for (uint32_t i = 0; i < tr_cnt; ++i)
+            ring[(tr_at + i) % S.TE] =
+                i < evicted ? make_uint2(0, 0) : sa[(tr_poff + i) % A];
+        }
       }
     }
 
@@ -666,6 +712,23 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       const uint32_t kept = cc < S.SC ? cc : S.SC;
       for (uint32_t i = cc - kept; i != cc; ++i) h = fnv(h, S.stream[(size_t)gi * S.SC + i % S.SC]);
     }
+    if (S.TC) {                                     // F3 trace rings, retained part
+      const uint32_t cnt = S.tcount[gi], kept = cnt < S.TC ? cnt : S.TC;
+      h = fnv(h, cnt);
+      for (uint32_t i = cnt - kept; i != cnt; ++i) {
+        const uint32_t* r = S.tr + ((size_t)gi * S.TC + i % S.TC) * 32;
+        for (int j = 0; j < 32; ++j) h = fnv(h, r[j]);
+      }
+    }
+    if (S.TE) {
+      const uint32_t cnt = S.tecount[gi], kept = cnt < S.TE ? cnt : S.TE;
+      h = fnv(h, cnt);
+      for (uint32_t i = cnt - kept; i != cnt; ++i) {
+        const uint2 e = S.tent[(size_t)gi * S.TE + i % S.TE];
+        h = fnv(h, e.x);
+        h = fnv(h, e.y);
+      }
+    }
     const uint32_t qh[2] = {qm & 15, (qm >> 9) & 15}, qc[2] = {(qm >> 4) & 31, (qm >> 13) & 31};
     for (int which = 0; which < 2; ++which) {
       h = fnv(h, qc[which]);
@@ -693,7 +756,10 @@ hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
   constexpr size_t lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
   const uint32_t waves = (S.C + CPW - 1) / CPW;
   const uint32_t blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL(tick_kernel<N>, dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  if (S.TC)
+    hipLaunchKernelGGL((tick_kernel<N, true>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+  else
+    hipLaunchKernelGGL((tick_kernel<N, false>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
   return hipGetLastError();
 }
 
@@ -715,7 +781,10 @@ template <int N>
 hipError_t configure_n() {
   constexpr int CPW = 64 / N;
   constexpr int lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N>),
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, false>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, true>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 

@@ -26,7 +26,8 @@ class Config(C.Structure):
                 ("part_ppm", C.c_uint32), ("part_epoch", C.c_uint32),
                 ("client_ppm", C.c_uint32), ("variant_flags", C.c_uint32),
                 ("device", C.c_int32), ("ticks_per_launch", C.c_uint32),
-                ("commit_stream_cap", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+                ("commit_stream_cap", C.c_uint32), ("trace_cap", C.c_uint32),
+                ("trace_entry_cap", C.c_uint32), ("reserved", C.c_uint32 * 1)]
 
 
 class Node(C.Structure):
@@ -59,6 +60,21 @@ class Msg(C.Structure):
 
 class Entry(C.Structure):
     _fields_ = [("term", C.c_uint32), ("val", C.c_uint32)]
+
+
+class TraceEvent(C.Structure):
+    _fields_ = [("tick", C.c_uint32), ("seq", C.c_uint32), ("msg", Msg),
+                ("role", C.c_uint8), ("voted_for", C.c_uint8), ("leader_id", C.c_uint8),
+                ("ls_present", C.c_uint8), ("votes", C.c_uint16), ("ls_keys", C.c_uint16),
+                ("current_term", C.c_uint32), ("next_index", C.c_int32 * MAX_NODES),
+                ("match_index", C.c_int32 * MAX_NODES), ("entries_seq", C.c_uint32)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["msg"] = {f: getattr(self.msg, f) for f, _ in Msg._fields_}
+        d["next_index"] = list(self.next_index)
+        d["match_index"] = list(self.match_index)
+        return d
 
 
 class Cluster(C.Structure):
@@ -102,6 +118,10 @@ _SIGS = {
                                      C.c_uint32]),
     "write_commit_stream": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32),
                                       C.c_uint32]),
+    "read_trace": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(TraceEvent),
+                             C.c_uint32]),
+    "read_trace_entries": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(Entry),
+                                     C.c_uint32]),
     "read_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
     "write_clusters": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Cluster)]),
     "read_counters": (C.c_int, [C.c_void_p, P(Counters)]),

@@ -154,6 +154,48 @@ class Backend:
         for i in range(1, self.N + 1):
             (d / f"node_{i}.log").write_text("".join(f"{v}\n" for v in self.commit_stream(cluster, i)))
 
+    def trace(self, cluster, node_id, first=0):
+        """F3: the node's recorded `wait` iterations with seq >= first (core.clj:182-186), oldest
+        first, as dicts of raft_trace_event_t fields."""
+        out, cap = [], max(1, self.config.trace_cap)
+        buf = (_abi.TraceEvent * cap)()
+        while True:
+            n = self._check(self._fns["read_trace"](self._h, cluster, node_id, first, buf, cap))
+            out.extend(buf[i].as_dict() for i in range(n))
+            if n < cap:
+                return out
+            first = out[-1]["seq"] + 1
+
+    def trace_entries(self, cluster, node_id, first, count):
+        """The `count` trace-entry-ring entries from index `first` as (term, val) pairs, or None
+        when the ring no longer holds them all (or trace_entry_cap is 0)."""
+        buf = (_abi.Entry * max(1, count))()
+        n = self._fns["read_trace_entries"](self._h, cluster, node_id, first, buf, count)
+        if n != count:
+            return None
+        return [(buf[i].term, buf[i].val) for i in range(n)]
+
+    def edn_trace(self, cluster, node_id, first=0, set_order="sorted"):
+        """The reference's stdout for node `node_id` of `cluster` from event `first` on:
+        `; Node` / (prn node) / `; Message` / (prn message) per wait (core.clj:182-186)."""
+        from . import edn
+        parts = []
+        for e in self.trace(cluster, node_id, first):
+            entries = None
+            if (e["msg"]["hdr"] & 7) == 2:
+                cnt = e["msg"]["hdr"] >> 16
+                entries = self.trace_entries(cluster, node_id, e["entries_seq"], cnt) if cnt else []
+            parts.append(edn.format_event(e, entries, node_id, self.N, set_order))
+        return "".join(parts)
+
+    def write_traces(self, directory, cluster=0, set_order="sorted"):
+        """One file per node, node_<id>.out, holding what that node's JVM prints per event."""
+        from pathlib import Path
+        d = Path(directory)
+        d.mkdir(parents=True, exist_ok=True)
+        for i in range(1, self.N + 1):
+            (d / f"node_{i}.out").write_text(self.edn_trace(cluster, i, set_order=set_order))
+
     def read_clusters(self, c0=0, nc=None):
         """Per-cluster records: checker high-water mark and client-injection cursor."""
         nc = self.C - c0 if nc is None else nc

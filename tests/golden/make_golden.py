@@ -15,8 +15,8 @@ import pyref  # noqa: E402
 
 CASES = {
     # BASELINE config 1: single 5-node cluster, seed 42, 10k ticks, no faults (full event trace)
-    "c1_seed42": dict(cfg=dict(nodes=5, seed=42), gid=0, ticks=10000, trace=True),
-    "c1_seed1": dict(cfg=dict(nodes=5, seed=1), gid=0, ticks=10000, trace=True),
+    "c1_seed42": dict(cfg=dict(nodes=5, seed=42), gid=0, ticks=10000, trace=True, stdout=True),
+    "c1_seed1": dict(cfg=dict(nodes=5, seed=1), gid=0, ticks=10000, trace=True, stdout=True),
     "faults_n5": dict(cfg=dict(nodes=5, seed=7, drop_ppm=100000, dup_ppm=20000, dmin=1, dmax=30,
                                part_ppm=100000, client_ppm=1500, log_cap=128), gid=3,
                       ticks=30000, trace=True),
@@ -38,14 +38,14 @@ class Tracer(pyref.PyCluster):
         for i in sorted(self.trace):
             if self.trace[i] != before[i]:
                 n = self.canonical_node(i)
-                self.events.append([t, i, n["role"], n["current_term"], n["fault"],
-                                    format(self.trace[i], "016x")])
+                self.hash_events.append([t, i, n["role"], n["current_term"], n["fault"],
+                                         format(self.trace[i], "016x")])
 
 
 def make(name, spec):
-    cfg = pyref.default_config(**spec["cfg"])
+    cfg = pyref.default_config(**spec["cfg"], trace_cap=1 if spec.get("stdout") else 0)
     c = Tracer(cfg, spec["gid"])
-    c.events = []
+    c.hash_events = []
     for t in range(spec["ticks"]):
         c.step(t)
     nodes = []
@@ -61,7 +61,9 @@ def make(name, spec):
            "counters": c.cnt,
            "first_violation_tick": c.first_violation}
     if spec["trace"]:
-        out["events"] = c.events
+        out["events"] = c.hash_events
+    if spec.get("stdout"):      # F3: what each node's `wait` prints (core.clj:182-186)
+        out["stdout"] = {str(i): pyref.stdout_of(c, i) for i in range(1, c.N + 1)}
     (HERE / f"{name}.json").write_text(json.dumps(out, separators=(",", ":")) + "\n")
     return out
 

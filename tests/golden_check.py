@@ -6,7 +6,7 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 NAMES = sorted(p.stem for p in GOLDEN.glob("*.json"))
 FIELDS = ["role", "voted_for", "leader_id", "fault", "entries_is_seq", "ls_present", "votes",
           "ls_keys", "current_term", "commit_index", "log_len", "deadline", "next_index",
-          "match_index", "last_led_term", "req_count", "res_count"]
+          "match_index", "last_led_term", "req_count", "res_count", "commit_count"]
 
 
 def load(name):
@@ -16,6 +16,8 @@ def load(name):
 def check(name, make):
     fx = load(name)
     cfg = dict(fx["config"], n_clusters=1, cluster_offset=fx["cluster_offset"])
+    if "stdout" in fx:
+        cfg.update(trace_cap=4096, trace_entry_cap=1 << 16)
     be = make(**cfg)
     N = cfg["nodes"]
     if "events" in fx:
@@ -54,6 +56,8 @@ def check(name, make):
     for k, v in fx["counters"].items():
         assert c[k] == v, (name, k, c[k], v)
     assert c["first_violation_tick"] == fx["first_violation_tick"]
+    for i, text in fx.get("stdout", {}).items():
+        assert be.edn_trace(0, int(i)) == text, (name, "stdout of node", i)
 
 
 def _first_diff(a, b):

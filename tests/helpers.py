@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+import re
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -54,6 +55,32 @@ def compare_py_backend(pc: "pyref.PyCluster", be: Backend, cluster: int):
                     A = len(ar)
                     assert [ar[(g[7] + k) % A] for k in range(pcnt)] == [tuple(e) for e in w[7]]
     assert be.read_clusters(cluster, 1)[0] == pc.canonical_cluster()
+    if be.config.trace_cap:
+        compare_trace(pc, be, cluster)
+
+
+def compare_trace(pc, be, cluster):
+    """F3: the backend's recorded wait events (and their printed form) equal pyref's."""
+    for i in range(1, pc.N + 1):
+        evs = pc.events[i]
+        first = max(0, len(evs) - be.config.trace_cap)
+        got = be.trace(cluster, i)
+        assert [e["seq"] for e in got] == list(range(first, len(evs))), f"node {i} trace seqs"
+        for e, (t, node, msg) in zip(got, evs[first:]):
+            assert e["tick"] == t, f"node {i} event {e['seq']} tick"
+            want = pyref.encode_msg(0, msg) if msg is not None else None
+            if want is None:
+                assert e["msg"]["hdr"] == 0 and e["msg"]["arrival"] == 0
+            else:
+                assert (e["msg"]["hdr"], e["msg"]["term"], e["msg"]["a"], e["msg"]["b"],
+                        e["msg"]["eterm"], e["msg"]["eval"]) == want[1:7], (i, e, msg)
+        got_txt, want_txt = be.edn_trace(cluster, i), pyref.stdout_of(pc, i, first)
+        if "#raft.sim/unretained" in got_txt:    # entries older than the trace-entry ring
+            want_txt = "\n".join(
+                re.sub(r":entries \[[^\]]*\]", lambda m: f":entries {unretained.pop(0)}", w)
+                if (unretained := re.findall(r"#raft.sim/unretained \d+", g)) else w
+                for g, w in zip(got_txt.split("\n"), want_txt.split("\n")))
+        assert got_txt == want_txt, f"node {i} EDN dump"
 
 
 def gpu(**cfg):

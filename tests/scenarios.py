@@ -30,7 +30,8 @@ class Scenario:
     def __init__(self, N, nodes, queues=None, hwm=(0, 0, 0), **cfg):
         self.N, self.nodes, self.hwm = N, nodes, hwm
         self.queues = queues or {}
-        self.cfg = dict(dict(nodes=N, n_clusters=1, log_cap=64, commit_stream_cap=64), **cfg)
+        self.cfg = dict(dict(nodes=N, n_clusters=1, log_cap=64, commit_stream_cap=64,
+                             trace_cap=64, trace_entry_cap=256), **cfg)
 
     # ---------------------------------------------------------------- C ABI backends
     def load_backend(self, make):
@@ -137,6 +138,9 @@ class PyView:
     def commit_stream(self, i):
         return list(self.pc.stream[i])
 
+    def edn(self, i):
+        return pyref.stdout_of(self.pc, i)
+
 
 class BackendView:
     def __init__(self, be):
@@ -156,6 +160,9 @@ class BackendView:
 
     def commit_stream(self, i):
         return self.be.commit_stream(0, i)
+
+    def edn(self, i):
+        return self.be.edn_trace(0, i)
 
 
 def run(scn, which, make=None):
@@ -382,6 +389,60 @@ def kat_client_set(view_of):
     assert v.node(2)["deadline"] >= 5000          # the event still re-arms the timer
 
 
+CHAN = "#<ManyToManyChannel clojure.core.async.impl.channels.ManyToManyChannel@%x>"
+
+
+def kat_printed_trace(view_of):
+    """What `wait` prints (core.clj:182-186) over a 3-node first election: the pre-handler node
+    map in init-node key order (core.clj:31-38), request bodies in the sender's literal order plus
+    :type and :resp-chan (core.clj:51-54,62-67; server.clj:14-21), replies {:term :id :type ..}
+    carrying the voter's own, never-updated term (core.clj:94,100)."""
+    nodes = {i: node(deadline=BIG) for i in range(1, 4)}
+    nodes[3] = node(deadline=0)
+    v = view_of(Scenario(3, nodes))
+    v.step(4)   # t0 timeout, t1 votes, t2 first grant -> leader (2 of 3), t3 second grant + AEs
+    rv = ("{:term 2, :candidate-id 3, :last-log-index 0, :last-log-term nil, "
+          ":type :request-vote, :resp-chan " + CHAN % 0 + "}")
+    assert v.edn(3) == (
+        "; Node\n"
+        "{:id 3, :state :follower, :current-term 1, :voted-for nil, :leader-id nil, "
+        ":leader-state nil, :votes #{}}\n"
+        "; Message\nnil\n\n"
+        "; Node\n"
+        "{:id 3, :state :candidate, :current-term 2, :voted-for 3, :leader-id nil, "
+        ":leader-state nil, :votes #{3}}\n"
+        "; Message\n{:term 1, :id 1, :type :vote-response, :vote-granted true}\n\n"
+        "; Node\n"
+        "{:id 3, :state :leader, :current-term 2, :voted-for nil, :leader-id 3, "
+        ":leader-state {:next-index {1 1, 2 1}, :match-index {1 0, 2 0}}, :votes #{}}\n"
+        "; Message\n{:term 1, :id 2, :type :vote-response, :vote-granted true}\n\n")
+    assert v.edn(1) == (
+        "; Node\n"
+        "{:id 1, :state :follower, :current-term 1, :voted-for nil, :leader-id nil, "
+        ":leader-state nil, :votes #{}}\n"
+        "; Message\n" + rv + "\n\n"
+        "; Node\n"
+        "{:id 1, :state :follower, :current-term 1, :voted-for 3, :leader-id nil, "
+        ":leader-state nil, :votes #{}}\n"
+        "; Message\n"
+        "{:term 2, :leader-id 3, :leader-commit 0, :prev-log-index 0, :prev-log-term nil, "
+        ":entries [], :type :append-entries, :resp-chan " + CHAN % 1 + "}\n\n")
+
+
+def kat_printed_entries(view_of):
+    """An append-entries prints its :entries (log.clj:67 shape) and its prev-log-term entry."""
+    ls = {2: (1, 0)}
+    nodes = {1: node("leader", term=2, leader_id=1, ls=ls, log=[E1, E2, E3], deadline=0,
+                     last_led=2),
+             2: node("follwer", term=2, leader_id=1, deadline=BIG)}
+    v = view_of(Scenario(2, nodes))
+    v.step(2)
+    assert v.edn(2).split("\n")[3] == (
+        "{:term 2, :leader-id 1, :leader-commit 0, :prev-log-index 0, "
+        ":prev-log-term {:term 2, :val 10}, :entries [{:term 2, :val 20} {:term 2, :val 30}], "
+        ":type :append-entries, :resp-chan " + CHAN % 0 + "}")
+
+
 ALL = [kat_majority, kat_first_election, kat_duplication, kat_truncate_crash, kat_cce, kat_npe,
        kat_partial_leader_state, kat_stale_step_down, kat_two_leaders_one_term, kat_vote_rules,
-       kat_variant_no_log_check, kat_client_set]
+       kat_variant_no_log_check, kat_client_set, kat_printed_trace, kat_printed_entries]

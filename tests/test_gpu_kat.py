@@ -47,5 +47,8 @@ class _Both:
     def commit_stream(self, i):
         return self.a.commit_stream(i)
 
+    def edn(self, i):
+        return self.a.edn(i)
+
     def counters(self):
         return self.a.counters()

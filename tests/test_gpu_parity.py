@@ -40,6 +40,11 @@ CASES = {
     "n4": dict(n_clusters=700, nodes=4, seed=23, client_ppm=500, **FAULTS),
     "n6": dict(n_clusters=700, nodes=6, seed=25, client_ppm=500, **FAULTS),
     "n8": dict(n_clusters=700, nodes=8, seed=27, client_ppm=500, **FAULTS),
+    # F3 trace rings on (they enter the digest): wrap-around, entry-ring overwrite, evictions
+    "traced": dict(n_clusters=1024, nodes=5, seed=31, client_ppm=2000, log_cap=128, trace_cap=48,
+                   trace_entry_cap=300, commit_stream_cap=16, **FAULTS),
+    "traced_tight": dict(n_clusters=256, nodes=9, seed=33, client_ppm=20000, log_cap=16,
+                         arena_cap=32, dup_ppm=100000, dmax=10, trace_cap=16, trace_entry_cap=64),
     "fast_timers": dict(n_clusters=1000, nodes=5, seed=29, hb=30, el_base=50, el_span=50,
                         client_ppm=20000, log_cap=128, **FAULTS),
 }
@@ -81,6 +86,23 @@ def test_gpu_c2_full_size():
     cfg = dict(n_clusters=65536, nodes=5, seed=42)
     g, r = run_pair(cfg, 10000, 10000)
     assert g.counters() == r.counters()
+
+
+def test_gpu_printed_trace_matches_oracle():
+    """F3: the `; Node` / `; Message` dump (core.clj:182-186) of GPU-recorded events equals the
+    oracle's, text for text, on a faulty client-driven run."""
+    cfg = dict(n_clusters=8, nodes=5, seed=35, client_ppm=3000, log_cap=256, trace_cap=4096,
+               trace_entry_cap=1 << 15, **FAULTS)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    g.step(20000)
+    r.step(20000)
+    n_entries = 0
+    for c in range(cfg["n_clusters"]):
+        for i in range(1, 6):
+            tg = g.edn_trace(c, i)
+            assert tg == r.edn_trace(c, i), (c, i)
+            n_entries += tg.count(":val ")
+    assert n_entries > 0
 
 
 def test_gpu_shard_invariance():

@@ -50,5 +50,8 @@ class _Both:
     def commit_stream(self, i):
         return self.py.commit_stream(i)
 
+    def edn(self, i):
+        return self.py.edn(i)
+
     def counters(self):
         return self.py.counters()

@@ -44,6 +44,8 @@ def random_config(rng):
     if rng.random() < 0.3:
         cfg["arena_cap"] = 2 * cfg["log_cap"]
     cfg["commit_stream_cap"] = rng.choice([0, 3, 64])
+    cfg["trace_cap"] = rng.choice([0, 3, 4096])
+    cfg["trace_entry_cap"] = 1 << 16 if cfg["trace_cap"] else 0
     return cfg
 
 
