@@ -43,7 +43,11 @@ enum raft_fault {
   RAFT_FAULT_OVERFLOW = 4  /* log capacity exceeded (simulator limit) */
 };
 
-enum raft_variant { RAFT_VARIANT_VOTE_NO_LOG_CHECK = 1 /* drop core.clj:96,99 */ };
+/* Bug-injection / correct-protocol flags (SIM_SPEC §4, §8). */
+enum raft_variant {
+  RAFT_VARIANT_VOTE_NO_LOG_CHECK = 1, /* drop core.clj:96,99 (with SPEC: drop the up-to-date check) */
+  RAFT_VARIANT_SPEC = 2               /* F4 Spec-Raft control: Raft Figure 2 rules (SIM_SPEC §8) */
+};
 
 /* Replaces `-main`'s argv (core.clj:197-200), the hard-coded timeouts (core.clj:173-174) and the
  * chan buffer sizes (server.clj:37, client.clj:18). Defaults: raft_sim_default_config(). */

@@ -339,9 +339,152 @@ def timeout_handler(rpc, log, cluster, node):                        # core.clj:
 
 
 # ----------------------------------------------------------------------------------------------
+# F4 Spec-Raft control (SIM_SPEC §8; variant flag 2). NOT reference behaviour: the rules of Figure 2
+# of the Raft paper on the same node maps, so that the faithful model above has a correct-protocol
+# control. Each function names the reference handler it replaces.
+# ----------------------------------------------------------------------------------------------
+def spec_majority(cluster, votes):                # strict majority (replaces core.clj:19-21)
+    return len(votes) >= (len(cluster) + 1) // 2 + 1
+
+
+def spec_step_down(node, term):                   # Raft "all servers": term > currentTerm
+    n = dict(node)
+    n.update({"state": ":follower", "current-term": term, "voted-for": None, "leader-id": None,
+              "leader-state": None, "votes": set()})
+    return n
+
+
+def spec_request_vote_rpc(rpc, log, cluster, node):          # replaces core.clj:48-54
+    last = log.entries[-1] if log.entries else None
+    msgs = [(p, {"type": "request-vote", "term": node["current-term"], "candidate-id": node["id"],
+                 "last-log-index": len(log.entries), "last-log-term": last}) for p in cluster]
+    for p, m in msgs:
+        rpc(p, m)
+
+
+def spec_append_entries_rpc(rpc, log, cluster, node):        # replaces core.clj:56-67
+    ls = node["leader-state"] or {"next-index": {}}
+    for p in cluster:
+        prev = min(max(s32(ls["next-index"].get(p, 0)) - 1, 0), len(log.entries))
+        rpc(p, {"type": "append-entries", "term": node["current-term"], "leader-id": node["id"],
+                "leader-commit": log.commit_index, "prev-log-index": prev,
+                "prev-log-term": log.entries[prev - 1] if prev else None,
+                "entries": list(log.entries[prev:])})
+
+
+def spec_request_vote_handler(log, message, node, respond, variant):   # replaces core.clj:91-103
+    term, cand = message["term"], message["candidate-id"]
+    if term > node["current-term"]:
+        node = spec_step_down(node, term)
+    lt = log.entries[-1][0] if log.entries else 0
+    mt = message["last-log-term"][0] if message["last-log-term"] is not None else 0
+    up_to_date = bool(variant & VOTE_NO_LOG_CHECK) or mt > lt or \
+        (mt == lt and message["last-log-index"] >= len(log.entries))
+    grant = term == node["current-term"] and node["voted-for"] in (None, cand) and up_to_date
+    respond({"term": node["current-term"], "id": node["id"], "type": "vote-response",
+             "vote-granted": grant})
+    if grant:
+        node = dict(node)
+        node["voted-for"] = cand
+    return node
+
+
+def spec_append_entries_handler(log, message, node, respond, stats):    # replaces core.clj:105-123
+    term, prev, ents = message["term"], message["prev-log-index"], message["entries"]
+    if term >= node["current-term"]:               # OVERFLOW is decided on the pre-event state
+        pt = message["prev-log-term"]
+        consistent = prev == 0 or (prev <= len(log.entries) and pt is not None
+                                   and log.entries[prev - 1][0] == pt[0])
+        if consistent:
+            check_capacity(log, prev + len(ents) - len(log.entries))
+    if term > node["current-term"]:
+        node = spec_step_down(node, term)
+    response = {"term": node["current-term"], "id": node["id"], "type": "append-response"}
+    if term < node["current-term"]:
+        respond(dict(response, success=False))
+        return node
+    n = dict(node)
+    n.update({"state": ":follower", "votes": set(), "leader-id": message["leader-id"],
+              "leader-state": None})
+    if not consistent:
+        respond(dict(response, success=False))
+        return n
+    k, hi = prev, min(len(log.entries), prev + len(ents))
+    while k < hi and log.entries[k][0] == ents[k - prev][0]:
+        k += 1
+    if k < prev + len(ents):                       # truncate at the first conflict, then append
+        stats["appended_at"] = k
+        stats["entries_appended"] += prev + len(ents) - k
+        log.entries = log.entries[:k] + list(ents[k - prev:])
+    old = log.commit_index
+    if message["leader-commit"] > old:
+        new = min(message["leader-commit"], prev + len(ents))
+        if new > old:
+            log.commit_index = new
+            stats["entries_applied"] += new - old
+            stats["written"] = [v for _, v in log.entries[old:new]]
+    respond(dict(response, success=True, commit=message["leader-commit"],
+                 **{"log-index": prev + len(ents)}))
+    return n
+
+
+def spec_vote_response_handler(rpc, log, cluster, message, node, stats):  # replaces core.clj:125-139
+    term, granted, id = message["term"], message["vote-granted"], message["id"]
+    if term > node["current-term"]:
+        return spec_step_down(node, term)
+    if term != node["current-term"] or not granted or node["state"] != ":candidate":
+        return node
+    votes = node["votes"] | {id}
+    n = dict(node)
+    if not spec_majority(cluster, votes):
+        n["votes"] = votes
+        return n
+    n.update({"state": ":leader", "votes": set(), "leader-id": node["id"],
+              "leader-state": {"next-index": {p: len(log.entries) + 1 for p in cluster},
+                               "match-index": {p: 0 for p in cluster}}})
+    spec_append_entries_rpc(rpc, log, cluster, n)
+    stats["elected"] = True
+    return n
+
+
+def spec_append_response_handler(log, cluster, message, node, stats):   # replaces core.clj:141-149
+    term, success, id = message["term"], message["success"], message["id"]
+    if term > node["current-term"]:
+        return spec_step_down(node, term)
+    if term != node["current-term"] or node["state"] != ":leader":
+        return node
+    ls = node["leader-state"]
+    n = dict(node)
+    n["leader-state"] = {"next-index": dict(ls["next-index"]),
+                         "match-index": dict(ls["match-index"])}
+    if not success:
+        n["leader-state"]["next-index"][id] = max(1, s32(ls["next-index"][id]) - 1)
+        return n
+    n["leader-state"]["next-index"][id] = message["log-index"] + 1
+    n["leader-state"]["match-index"][id] = message["log-index"]
+    stats["match_changed"] = True
+    vals = sorted([len(log.entries)] + [s32(n["leader-state"]["match-index"][p]) for p in cluster],
+                  reverse=True)
+    m = min(vals[(len(cluster) + 1) // 2], len(log.entries))     # the maj-th largest
+    old = log.commit_index
+    if m > old and log.entries[m - 1][0] == n["current-term"]:
+        log.commit_index = m
+        stats["entries_applied"] += m - old
+        stats["written"] = [v for _, v in log.entries[old:m]]
+    return n
+
+
+def spec_timeout_handler(rpc, log, cluster, node):                     # replaces core.clj:166-169
+    new_node = follower_to_candidate(node)
+    spec_request_vote_rpc(rpc, log, cluster, new_node)
+    return new_node
+
+
+# ----------------------------------------------------------------------------------------------
 # Tick engine (SIM_SPEC §4): the lockstep restatement of wait (core.clj:176-195)
 # ----------------------------------------------------------------------------------------------
 VOTE_NO_LOG_CHECK = 1
+SPEC = 2
 
 TYPE_CODE = {"request-vote": 1, "append-entries": 2, "client-set": 3,
              "vote-response": 4, "append-response": 5}
@@ -500,14 +643,36 @@ class PyCluster:
             stats = {"entries_appended": 0, "entries_applied": 0, "appended_at": None,
                      "elected": False, "match_changed": False, "written": []}
             cluster = self.cluster[i]
+            spec = bool(cfg["variant_flags"] & SPEC)
             try:
-                if msg is None:
+                if msg is None and spec:
+                    if node["state"] == ":leader":
+                        ev = 7
+                        spec_append_entries_rpc(rpc, log, cluster, node)
+                        new = node
+                    else:
+                        ev = 6
+                        new = spec_timeout_handler(rpc, log, cluster, node)
+                elif msg is None:
                     if node["state"] == ":leader":
                         ev = 7
                         new = heartbeat_handler(rpc, log, cluster, node)
                     else:
                         ev = 6
                         new = timeout_handler(rpc, log, cluster, node)
+                elif spec:
+                    ev = TYPE_CODE[msg["type"]]
+                    if ev == 1:
+                        new = spec_request_vote_handler(log, msg, node, respond,
+                                                        cfg["variant_flags"])
+                    elif ev == 2:
+                        new = spec_append_entries_handler(log, msg, node, respond, stats)
+                    elif ev == 3:
+                        new = client_set_handler(log, msg, node, stats)
+                    elif ev == 4:
+                        new = spec_vote_response_handler(rpc, log, cluster, msg, node, stats)
+                    else:
+                        new = spec_append_response_handler(log, cluster, msg, node, stats)
                 else:
                     ev = TYPE_CODE[msg["type"]]
                     if ev == 1:
@@ -598,7 +763,11 @@ class PyCluster:
             li = self.logs[i].entries
             vals = [len(li)] + [s32(ls["match-index"].get(p, 0)) for p in self.cluster[i]]
             vals.sort(reverse=True)
-            m = min(vals[(N + 1) // 2 - 1], len(li))
+            spec = bool(self.cfg["variant_flags"] & SPEC)
+            maj = N // 2 + 1 if spec else (N + 1) // 2
+            m = min(vals[maj - 1], len(li))
+            if spec and m > 0 and li[m - 1][0] != node["current-term"]:
+                continue                 # SIM_SPEC §8: not committed under Raft's rule
             if m > self.hwm[0] and (best is None or m > best[0]):
                 best = (m, li[m - 1][0], li[m - 1][1])
         if best is not None:

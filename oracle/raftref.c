@@ -113,6 +113,7 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->part_epoch < 1) return fail(-EINVAL, "part_epoch must be >= 1");
   if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
       c->client_ppm > 1000000) return fail(-EINVAL, "ppm values must be <= 1e6");
+  if (c->variant_flags & ~3u) return fail(-EINVAL, "variant_flags: only bits 0-1 are defined");
   if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
     return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
   return 0;
@@ -192,7 +193,7 @@ typedef struct { int n; uint32_t arr[2]; raft_msg_t m; } cell_t;
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 typedef struct {
   int kind, reloc;
-  uint32_t old_base, old_len, src, poff, pcnt, applied;
+  uint32_t old_base, old_len, src, poff, pcnt, applied, apply_from;
   raft_entry_t entry;
 } plan_t;
 
@@ -342,6 +343,43 @@ static uint64_t trace(uint64_t h, uint32_t t, uint32_t ev, uint32_t src, uint32_
 
 static uint32_t popcount16(uint32_t v) { return (uint32_t)__builtin_popcount(v & 0xFFFF); }
 
+/* ---------------------------------------------------------------- F4 Spec-Raft (SIM_SPEC §8)
+ * NOT reference behaviour: Raft Figure 2 rules on the same state, the correct-protocol control. */
+
+/* "All servers: if RPC term > currentTerm, set currentTerm = term, convert to follower". */
+static void spec_step_down(raft_node_t* nn, uint32_t term) {
+  nn->current_term = term; nn->voted_for = 0; nn->votes = 0; nn->leader_id = 0;
+  nn->role = RAFT_FOLLOWER;
+  if (nn->ls_present) {
+    nn->ls_present = 0; nn->ls_keys = 0;
+    memset(nn->next_index, 0, sizeof nn->next_index);
+    memset(nn->match_index, 0, sizeof nn->match_index);
+  }
+}
+
+/* AppendEntries to every peer: prev = next-1 (clamped to the log), prev-log-term = entry prev,
+ * entries [prev, len) (replaces append-entries-rpc, core.clj:56-67). */
+static void spec_ae_broadcast(tick_ctx_t* x, uint32_t k, const raft_node_t* nn, emit_t* em,
+                              int* ne) {
+  uint32_t id = k + 1;
+  const raft_entry_t* ar = arena_of(x->s, x->c * x->N + k);
+  for (uint32_t p = 1; p <= x->N; ++p) {
+    if (p == id) continue;
+    int32_t pv = nn->next_index[p - 1] - 1;
+    uint32_t prev = pv <= 0 ? 0u : ((uint32_t)pv < nn->log_len ? (uint32_t)pv : nn->log_len);
+    raft_msg_t m = {0};
+    m.term = nn->current_term; m.a = nn->commit_index; m.b = prev;
+    uint32_t ep = 0, pcnt = nn->log_len - prev;
+    if (prev) {
+      raft_entry_t pe = ar[(nn->arena_base + prev - 1) % x->s->A];
+      ep = 1; m.eterm = pe.term; m.eval = pe.val;
+    }
+    m.poff = pcnt ? nn->arena_base + prev : 0;
+    m.hdr = hdr(RAFT_MSG_APPEND_ENTRIES, id, 0, ep, pcnt);
+    em[*ne].dst = p; em[*ne].m = m; (*ne)++;
+  }
+}
+
 static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc) {
   const raft_sim_config_t* cfg = &s->cfg;
   tick_ctx_t X;
@@ -381,6 +419,11 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
   const uint32_t h_index = cr->hwm_index, h_term = cr->hwm_term, h_val = cr->hwm_val;
   memset(plan, 0, sizeof plan);
   for (uint32_t k = 0; k < N; ++k) appended_at[k] = -1;
+
+  /* pre-tick arena frontiers (Spec-Raft reads payloads in P1 against them, SIM_SPEC §8) */
+  const int spec = (cfg->variant_flags & RAFT_VARIANT_SPEC) != 0;
+  uint32_t front0[RAFT_MAX_NODES];
+  for (uint32_t k = 0; k < N; ++k) front0[k] = x->nodes[k].arena_frontier;
 
   /* P1 one event per running node (wait, core.clj:176-195) */
   for (uint32_t k = 0; k < N; ++k) {
@@ -431,7 +474,163 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
     uint64_t appended = 0, applied = 0;
     uint32_t type = m.hdr & 7, src = (m.hdr >> 3) & 15, flag = (m.hdr >> 7) & 1;
     uint32_t pcnt = m.hdr >> 16;
-    if (which < 0) {
+    const raft_entry_t* own = arena_of(s, gi);
+    if (spec && which < 0) {
+      if (n->role == RAFT_LEADER) {                                  /* heartbeat */
+        ev = 7;
+        spec_ae_broadcast(x, k, &nn, em, &ne);
+      } else {                                                       /* election timeout */
+        ev = 6;
+        nn.role = RAFT_CANDIDATE; nn.voted_for = (uint8_t)id;
+        nn.votes = (uint16_t)(1u << id); nn.current_term = n->current_term + 1;
+        raft_msg_t r = {0};
+        uint32_t ep = 0;
+        r.term = nn.current_term; r.a = n->log_len;
+        if (n->log_len) {
+          raft_entry_t e = own[(n->arena_base + n->log_len - 1) % s->A];
+          ep = 1; r.eterm = e.term; r.eval = e.val;
+        }
+        r.hdr = hdr(RAFT_MSG_REQUEST_VOTE, id, 0, ep, 0);
+        for (uint32_t p = 1; p <= N; ++p)
+          if (p != id) { em[ne].dst = p; em[ne].m = r; ne++; }
+      }
+    } else if (spec) {
+      ev = type; msrc = src; mterm = m.term;
+      raft_msg_t r = {0};
+      int consistent = 0;
+      /* OVERFLOW, the only Spec-Raft halt, is decided on the pre-event state */
+      if (type == RAFT_MSG_APPEND_ENTRIES && m.term >= n->current_term) {
+        consistent = m.b == 0 || (m.b <= n->log_len && ((m.hdr >> 8) & 1) &&
+                                  own[(n->arena_base + m.b - 1) % s->A].term == m.eterm);
+        if (consistent && (uint64_t)m.b + pcnt > s->L) fault = RAFT_FAULT_OVERFLOW;
+      }
+      if (type == RAFT_MSG_CLIENT_SET && n->role == RAFT_LEADER && n->log_len + 1 > s->L)
+        fault = RAFT_FAULT_OVERFLOW;
+      if (!fault && type != RAFT_MSG_CLIENT_SET && m.term > nn.current_term)
+        spec_step_down(&nn, m.term);
+      switch (fault ? 0 : type) {
+        case RAFT_MSG_REQUEST_VOTE: {
+          uint32_t lt = n->log_len ? own[(n->arena_base + n->log_len - 1) % s->A].term : 0;
+          uint32_t mt = ((m.hdr >> 8) & 1) ? m.eterm : 0;
+          int up = (cfg->variant_flags & RAFT_VARIANT_VOTE_NO_LOG_CHECK) || mt > lt ||
+                   (mt == lt && m.a >= n->log_len);
+          int grant = m.term == nn.current_term &&
+                      (nn.voted_for == 0 || nn.voted_for == src) && up;
+          if (grant) nn.voted_for = (uint8_t)src;
+          r.term = nn.current_term;
+          r.hdr = hdr(RAFT_MSG_VOTE_RESPONSE, id, (uint32_t)grant, 0, 0);
+          em[ne].dst = src; em[ne].m = r; ne++;
+          break;
+        }
+        case RAFT_MSG_APPEND_ENTRIES: {
+          r.term = nn.current_term;
+          r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 0, 0, 0);
+          if (m.term < nn.current_term) { em[ne].dst = src; em[ne].m = r; ne++; break; }
+          nn.role = RAFT_FOLLOWER; nn.votes = 0; nn.leader_id = (uint8_t)src;
+          if (nn.ls_present) {
+            nn.ls_present = 0; nn.ls_keys = 0;
+            memset(nn.next_index, 0, sizeof nn.next_index);
+            memset(nn.match_index, 0, sizeof nn.match_index);
+          }
+          if (!consistent) { em[ne].dst = src; em[ne].m = r; ne++; break; }
+          /* first conflict in [b, min(len, b+pcnt)); payload read from the sender's arena with
+             eviction judged by its pre-tick frontier */
+          const raft_entry_t* sa = arena_of(s, c * N + src - 1);
+          uint32_t kk = m.b, hi = n->log_len < m.b + pcnt ? n->log_len : m.b + pcnt;
+          for (; kk < hi; ++kk) {
+            uint32_t i = kk - m.b, pt = 0;
+            if ((uint64_t)front0[src - 1] > (uint64_t)m.poff + i + s->A)
+              lc->c[RAFT_CTR_PAYLOAD_EVICTED]++;
+            else
+              pt = sa[(m.poff + i) % s->A].term;
+            if (own[(n->arena_base + kk) % s->A].term != pt) break;
+          }
+          uint32_t mc = m.b + pcnt - kk;
+          if (mc) {                      /* truncate at kk, append payload [kk-b, pcnt) */
+            plan[k].kind = PLAN_PAYLOAD; plan[k].src = src;
+            plan[k].poff = m.poff + (kk - m.b); plan[k].pcnt = mc;
+            plan[k].old_base = nn.arena_base; plan[k].old_len = kk; plan[k].reloc = 0;
+            if (kk < nn.log_len || nn.arena_base + nn.log_len != nn.arena_frontier) {
+              plan[k].reloc = 1;
+              nn.arena_base = nn.arena_frontier;
+              nn.arena_frontier += kk;
+            }
+            nn.arena_frontier += mc;
+            nn.log_len = m.b + pcnt;
+            appended = mc;
+            appended_at[k] = (int)kk;
+          }
+          if (m.a > nn.commit_index) {
+            uint32_t nc = m.a < m.b + pcnt ? m.a : m.b + pcnt;
+            if (nc > nn.commit_index) {
+              applied = nc - nn.commit_index;
+              plan[k].applied = (uint32_t)applied; plan[k].apply_from = nn.commit_index;
+              nn.commit_index = nc;
+            }
+          }
+          r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 1, 0, 0);
+          r.a = m.a; r.b = m.b + pcnt;
+          em[ne].dst = src; em[ne].m = r; ne++;
+          break;
+        }
+        case RAFT_MSG_CLIENT_SET: {                     /* as client-set-handler 151-160 */
+          if (n->role != RAFT_LEADER) break;
+          plan[k].kind = PLAN_ENTRY;
+          plan[k].entry.term = n->current_term; plan[k].entry.val = m.a;
+          plan_append(x, &nn, &plan[k], 1);
+          appended = 1;
+          appended_at[k] = (int)n->log_len;
+          break;
+        }
+        case RAFT_MSG_VOTE_RESPONSE: {
+          if (m.term != nn.current_term || !flag || nn.role != RAFT_CANDIDATE) break;
+          uint32_t votes = nn.votes | (1u << src);
+          if (popcount16(votes) < N / 2 + 1) { nn.votes = (uint16_t)votes; break; }
+          nn.role = RAFT_LEADER; nn.votes = 0; nn.leader_id = (uint8_t)id;   /* voted_for kept */
+          nn.ls_present = 1; nn.ls_keys = 0;
+          for (uint32_t p = 1; p <= N; ++p) {
+            nn.next_index[p - 1] = 0; nn.match_index[p - 1] = 0;
+            if (p == id) continue;
+            nn.ls_keys |= (uint16_t)(1u << p);
+            nn.next_index[p - 1] = (int32_t)(nn.log_len + 1);
+          }
+          spec_ae_broadcast(x, k, &nn, em, &ne);
+          elect = 1;
+          break;
+        }
+        case RAFT_MSG_APPEND_RESPONSE: {
+          if (m.term != nn.current_term || nn.role != RAFT_LEADER) break;
+          if (!flag) {
+            int32_t nx = nn.next_index[src - 1] - 1;
+            nn.next_index[src - 1] = nx > 1 ? nx : 1;
+            break;
+          }
+          nn.next_index[src - 1] = (int32_t)(m.b + 1);
+          nn.match_index[src - 1] = (int32_t)m.b;
+          mchg = 1;
+          int32_t vals[RAFT_MAX_NODES];
+          uint32_t nv = 0;
+          vals[nv++] = (int32_t)nn.log_len;
+          for (uint32_t p = 1; p <= N; ++p)
+            if (p != id) vals[nv++] = nn.match_index[p - 1];
+          for (uint32_t i = 1; i < nv; ++i)          /* sort descending */
+            for (uint32_t j = i; j > 0 && vals[j - 1] < vals[j]; --j) {
+              int32_t tmp = vals[j]; vals[j] = vals[j - 1]; vals[j - 1] = tmp;
+            }
+          int32_t mm = vals[N / 2];                    /* the maj-th largest */
+          if (mm > (int32_t)nn.log_len) mm = (int32_t)nn.log_len;
+          if (mm > (int32_t)nn.commit_index &&
+              own[(nn.arena_base + (uint32_t)mm - 1) % s->A].term == nn.current_term) {
+            applied = (uint32_t)mm - nn.commit_index;
+            plan[k].applied = (uint32_t)applied; plan[k].apply_from = nn.commit_index;
+            nn.commit_index = (uint32_t)mm;
+          }
+          break;
+        }
+        default:
+          break;
+      }
+    } else if (which < 0) {
       if (n->role == RAFT_LEADER) {                          /* heartbeat-handler 162-164 */
         ev = 7;
         fault = ae_broadcast(x, k, &nn, em, &ne);
@@ -490,6 +689,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
             nn.commit_index = nn.log_len;
             applied = nn.commit_index > oldc ? nn.commit_index - oldc : 0;
             plan[k].applied = (uint32_t)applied;
+            plan[k].apply_from = oldc;
             r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 1, 0, 0);
             r.a = m.a; r.b = m.b + pcnt;
             nn.role = RAFT_FOLLWER; nn.voted_for = 0; nn.votes = 0; /* candidate->follower */
@@ -644,7 +844,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
     raft_node_t* n = &x->nodes[k];
     const raft_entry_t* ar = arena_of(s, c * N + k);
     uint32_t* ring = s->stream + (size_t)(c * N + k) * (s->S ? s->S : 1);
-    for (uint32_t i = n->log_len - a; i < n->log_len; ++i) {
+    for (uint32_t i = plan[k].apply_from; i < plan[k].apply_from + a; ++i) {
       if (s->S) ring[n->commit_count % s->S] = ar[(n->arena_base + i) % s->A].val;
       n->commit_count++;
     }
@@ -700,8 +900,12 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
         for (uint32_t j = i; j > 0 && vals[j - 1] < vals[j]; --j) {
           int32_t tmp = vals[j]; vals[j] = vals[j - 1]; vals[j - 1] = tmp;
         }
-      int32_t mm = vals[(N + 1) / 2 - 1];
+      int32_t mm = vals[(spec ? N / 2 + 1 : (N + 1) / 2) - 1];
       if (mm > (int32_t)nk->log_len) mm = (int32_t)nk->log_len;
+      /* Spec-Raft (SIM_SPEC §8): only an entry of the leader's own term is committed by count */
+      if (spec && mm > 0 &&
+          arena_of(s, c * N + k)[(nk->arena_base + (uint32_t)mm - 1) % s->A].term != nk->current_term)
+        continue;
       if (mm > (int32_t)h_index && mm > best) {
         best = mm;
         raft_entry_t e = arena_of(s, c * N + k)[(nk->arena_base + (uint32_t)mm - 1) % s->A];

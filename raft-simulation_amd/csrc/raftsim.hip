@@ -73,6 +73,7 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->drop_ppm > 1000000 || c->dup_ppm > 1000000 || c->part_ppm > 1000000 ||
       c->client_ppm > 1000000)
     return fail(-EINVAL, "ppm values must be <= 1e6");
+  if (c->variant_flags & ~3u) return fail(-EINVAL, "variant_flags: only bits 0-1 are defined");
   if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
     return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
   return 0;

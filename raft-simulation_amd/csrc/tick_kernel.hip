@@ -136,8 +136,13 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   };
   uint32_t wnext = next_event();
 
-  for (uint32_t t = t0; t != t0 + nt; ++t) {
-    if (t < wnext) continue;                   // idle tick for every cluster of this wave
+  const uint32_t tend = t0 + nt;
+  for (uint32_t t = t0;; ++t) {
+    // Ticks before the wave's next event change nothing (every handler, injection and delivery
+    // is keyed to a deadline, a queue head or the injection cursor, all folded into wnext), so
+    // the wave jumps over them: discrete-event skipping with tick-exact results.
+    if (t < wnext) t = wnext < tend ? wnext : tend;
+    if (t == tend) break;
     const bool live = active && !n.fault;
     // Opaque per-tick copy of the node index: keeps the compiler from hoisting every address
     // the event path might use out of the tick loop (that costs ~30 loop-carried VGPRs).
