@@ -84,12 +84,197 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-template <int N, bool TRACE>
+// F4 Spec-Raft control (SIM_SPEC §8): one event of a running node under Raft's Figure 2 rules.
+// NOT reference behaviour. Same contract as the faithful handler below it in tick_kernel: decide
+// `fault` (OVERFLOW only) before touching the node, then mutate `n` in place and describe the
+// emission (emit/ra/rb), the leader-state writes (nm) and the P3 log plan.
+template <int N, uint32_t MAJ>
+__device__ __forceinline__ void spec_handle(
+    const DevSim& S, NodeR& n, const uint2* sar, const uint32_t* fr, uint32_t* lctr, int which,
+    uint32_t id, int k, int bl, uint32_t sgi, uint32_t peers, uint4 m0, uint4 m1,
+    uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
+    uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
+    uint32_t& pold_base, uint32_t& pold_len, uint32_t& preloc, uint32_t& pet, uint32_t& pev,
+    uint32_t& papplied, uint32_t& papply_from, int& appended_at, bool& elected, bool& mchg) {
+  const uint32_t A = S.A, NN = S.NN;
+  if (which < 0) {
+    if (n.role == RAFT_LEADER) {                                  // heartbeat
+      ev = 7;
+      emit = 2;
+    } else {                                                      // election timeout
+      ev = 6;
+      uint32_t ep = 0, et = 0, evl = 0;
+      if (n.len) {
+        const uint2 e = sar[(n.base + n.len - 1) % A];
+        ep = 1; et = e.x; evl = e.y;
+      }
+      n.role = RAFT_CANDIDATE; n.vf = id; n.votes = 1u << id; n.term += 1;
+      ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, n.term, n.len, 0);
+      rb = make_uint4(et, evl, 0, 0);
+      emit = 1;
+    }
+    return;
+  }
+  const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mpoff = m1.w;
+  const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
+                 mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
+  ev = type;
+  // OVERFLOW, the only Spec-Raft halt, is decided on the pre-event state
+  bool consistent = false;
+  if (type == RAFT_MSG_APPEND_ENTRIES && mterm >= n.term) {
+    consistent = mb == 0;
+    if (!consistent && mb <= n.len && mep) consistent = sar[(n.base + mb - 1) % A].x == met;
+    if (consistent && mb + pcnt > S.L) fault = RAFT_FAULT_OVERFLOW;
+  }
+  if (type == RAFT_MSG_CLIENT_SET && n.role == RAFT_LEADER && n.len + 1 > S.L)
+    fault = RAFT_FAULT_OVERFLOW;
+  if (fault) return;
+  if (type != RAFT_MSG_CLIENT_SET && mterm > n.term) {          // term rule: step down
+    n.term = mterm; n.vf = 0; n.votes = 0; n.lid = 0; n.role = RAFT_FOLLOWER;
+    if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
+  }
+  switch (type) {
+    case RAFT_MSG_REQUEST_VOTE: {
+      const uint32_t lt = n.len ? sar[(n.base + n.len - 1) % A].x : 0u;
+      const uint32_t mt = mep ? met : 0u;
+      const bool up = (S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) || mt > lt ||
+                      (mt == lt && ma >= n.len);
+      const uint32_t grant = mterm == n.term && (n.vf == 0 || n.vf == src) && up;
+      ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
+      if (grant) n.vf = src;
+      emit = 3;
+      break;
+    }
+    case RAFT_MSG_APPEND_ENTRIES: {
+      ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
+      emit = 3;
+      if (mterm < n.term) break;
+      n.role = RAFT_FOLLOWER; n.votes = 0; n.lid = src;
+      if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
+      if (!consistent) break;
+      // first conflict in [b, min(len, b + pcnt)); the payload is read from the sender's arena,
+      // an entry its pre-tick frontier has overwritten reading (0, 0)
+      const uint64_t sf0 = fr[bl + (int)src - 1];
+      const uint2* sa = arena_of(S, sgi - k + src - 1);
+      const uint32_t hi = n.len < mb + pcnt ? n.len : mb + pcnt;
+      uint32_t kk = mb, evc = 0;
+      for (; kk < hi; ++kk) {
+        const uint32_t i = kk - mb;
+        uint32_t pt = 0;
+        if (sf0 > (uint64_t)mpoff + i + A) ++evc;
+        else pt = sa[(mpoff + i) % A].x;
+        if (sar[(n.base + kk) % A].x != pt) break;
+      }
+      lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evc);
+      const uint32_t mc = mb + pcnt - kk;
+      if (mc) {                               // truncate at kk, append payload [kk - b, pcnt)
+        pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff + (kk - mb); ppcnt = mc;
+        pold_base = n.base; pold_len = kk;
+        if (kk < n.len || n.base + n.len != n.front) {
+          preloc = 1;
+          n.base = n.front;
+          n.front += kk;
+        }
+        n.front += mc;
+        appended_at = (int)kk;
+        n.len = mb + pcnt;
+        appended = mc;
+      }
+      if (ma > n.commit) {
+        const uint32_t nc = ma < mb + pcnt ? ma : mb + pcnt;
+        if (nc > n.commit) {
+          applied = nc - n.commit; papplied = applied; papply_from = n.commit;
+          n.commit = nc;
+        }
+      }
+      ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
+      break;
+    }
+    case RAFT_MSG_CLIENT_SET: {                                   // as client-set-handler 151-160
+      if (n.role != RAFT_LEADER) break;
+      pkind = PLAN_ENTRY; pet = n.term; pev = ma;
+      pold_base = n.base; pold_len = n.len;
+      if (n.base + n.len != n.front) {
+        preloc = 1;
+        n.base = n.front;
+        n.front += n.len;
+      }
+      n.front += 1;
+      appended_at = (int)n.len;
+      n.len += 1;
+      n.seq = 0;
+      appended = 1;
+      break;
+    }
+    case RAFT_MSG_VOTE_RESPONSE: {
+      if (mterm != n.term || !flag || n.role != RAFT_CANDIDATE) break;
+      const uint32_t votes = n.votes | 1u << src;
+      if (__popc(votes) < MAJ) {
+        n.votes = votes;
+        break;
+      }
+      n.role = RAFT_LEADER; n.votes = 0; n.lid = id;              // voted_for kept
+      n.lsp = 1; n.keys = peers;
+      nm = 1;
+      emit = 2;
+      elected = true;
+      break;
+    }
+    case RAFT_MSG_APPEND_RESPONSE: {
+      if (mterm != n.term || n.role != RAFT_LEADER) break;
+      if (!flag) {
+        nm = 3;
+        break;
+      }
+      nm = 4;
+      mchg = true;
+      // majority commit: the MAJ-th largest of {log_len} ∪ match_index (own slot holds log_len),
+      // by an unrolled compare-exchange network
+      int32_t vals[N];
+#pragma unroll
+      for (int p = 1; p <= N; ++p)
+        vals[p - 1] = p == (int)id ? (int32_t)n.len
+                                   : (p == (int)src ? (int32_t)mb : S.match[(p - 1) * NN + sgi]);
+#pragma unroll
+      for (int i = 1; i < N; ++i)
+#pragma unroll
+        for (int q = i; q > 0; --q)
+          if (vals[q - 1] < vals[q]) {
+            const int32_t tmp = vals[q]; vals[q] = vals[q - 1]; vals[q - 1] = tmp;
+          }
+      int32_t mm = vals[MAJ - 1];
+      if (mm > (int32_t)n.len) mm = (int32_t)n.len;
+      if (mm > (int32_t)n.commit && sar[(n.base + (uint32_t)mm - 1) % A].x == n.term) {
+        applied = (uint32_t)mm - n.commit; papplied = applied; papply_from = n.commit;
+        n.commit = (uint32_t)mm;
+      }
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+// LDS words per wave: message cells [cluster][sender][receiver], counters, and (Spec-Raft) the
+// wave's pre-tick arena frontiers.
+template <int N, bool SPEC>
+constexpr int wave_lds_words() {
+  return (64 / N) * N * N * 8 + LCTR_WORDS + (SPEC ? 64 : 0);
+}
+template <int N, bool SPEC>
+constexpr size_t block_lds_bytes() {
+  return (PW_WORDS + 4 * wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
+}
+
+// SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
+// faithful kernel carries none of its code.
+template <int N, bool TRACE, bool SPEC>
 __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr int CELL_WORDS = CPW * N * N * 8;
-  constexpr int WAVE_WORDS = CELL_WORDS + LCTR_WORDS;
+  constexpr int WAVE_WORDS = wave_lds_words<N, SPEC>();
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
+  constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // block-shared: the client-gap power table (SIM_SPEC P0), then one region per wave
@@ -98,6 +283,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   __syncthreads();
   uint32_t* cells = smem + PW_WORDS + wv * WAVE_WORDS;
   uint32_t* lctr = cells + CELL_WORDS;
+  uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
   const uint32_t wave = blockIdx.x * 4 + wv;
@@ -149,6 +335,10 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     uint32_t sgi = gi, sg = g;
     asm volatile("" : "+v"(sgi), "+v"(sg));
     uint2* const sar = arena_of(S, sgi);
+    if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
+      fr[lane] = n.front;
+      __builtin_amdgcn_wave_barrier();
+    }
 
     // ---------------------------------------------------------------- P0 client injection (D9)
     bool inj = false;
@@ -184,7 +374,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     const bool res_ok = live && n.rs.arr <= t;
     uint32_t sentmask = 0;
     uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, pold_len = 0,
-             preloc = 0, pet = 0, pev = 0, papplied = 0;
+             preloc = 0, pet = 0, pev = 0, papplied = 0, papply_from = 0;
     int appended_at = -1;
     bool elected = false, mchg = false;
     uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
@@ -240,7 +430,12 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);  // reply cell words
       uint32_t appended = 0, applied = 0;
 
-      if (which < 0) {
+      if constexpr (SPEC) {
+        spec_handle<N, MAJ>(S, n, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
+                            emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
+                            pold_base, pold_len, preloc, pet, pev, papplied, papply_from,
+                            appended_at, elected, mchg);
+      } else if (which < 0) {
         if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
           ev = 7;
           // append-entries-rpc (core.clj:56-67): last-entry, then per peer in doseq order
@@ -326,6 +521,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
               n.commit = n.len;                              // apply-entries! 69-76
               applied = n.commit > oldc ? n.commit - oldc : 0;
               papplied = applied;
+              papply_from = oldc;
               n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;  // candidate->follower 75-78
               n.lid = src; n.term = mterm;
             }
@@ -419,16 +615,22 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
         // leader-state words (cold, in HBM)
         if (nm == 1 || nm == 2) {
+          const int32_t first_next = (int32_t)((SPEC ? n.len : n.commit) + 1);
 #pragma unroll
           for (int p = 1; p <= N; ++p) {
-            S.next[(p - 1) * NN + sgi] = (nm == 1 && p != (int)id) ? (int32_t)(n.commit + 1) : 0;
+            S.next[(p - 1) * NN + sgi] = (nm == 1 && p != (int)id) ? first_next : 0;
             S.match[(p - 1) * NN + sgi] = 0;
           }
         } else if (nm == 3) {
-          S.next[(src - 1) * NN + sgi] -= 1;
+          if constexpr (SPEC) {
+            const int32_t nx = S.next[(src - 1) * NN + sgi] - 1;
+            S.next[(src - 1) * NN + sgi] = nx > 1 ? nx : 1;
+          } else {
+            S.next[(src - 1) * NN + sgi] -= 1;
+          }
         } else if (nm == 4) {
-          S.next[(src - 1) * NN + sgi] = (int32_t)mb;
-          S.match[(src - 1) * NN + sgi] = (int32_t)ma;
+          S.next[(src - 1) * NN + sgi] = (int32_t)(SPEC ? mb + 1 : mb);
+          S.match[(src - 1) * NN + sgi] = (int32_t)(SPEC ? mb : ma);
         }
         lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
@@ -453,7 +655,19 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
-              if (emit == 2) {
+              if (SPEC && emit == 2) {                    // SIM_SPEC §8 broadcast
+                const int32_t pv = S.next[(p - 1) * NN + sgi] - 1;
+                const uint32_t prev = pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
+                uint32_t ep = 0, et = 0, evl = 0;
+                if (prev) {
+                  const uint2 e = sar[(n.base + prev - 1) % A];
+                  ep = 1; et = e.x; evl = e.y;
+                }
+                const uint32_t pc = n.len - prev;
+                ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
+                                n.commit, prev);
+                rb = make_uint4(et, evl, pc ? n.base + prev : 0, 0);
+              } else if (emit == 2) {
                 const int32_t nx = S.next[(p - 1) * NN + sgi];
                 const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
                 const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
@@ -507,7 +721,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     }
 
     // ---------------------------------------------------------------- P3 log writes
-    if (__ballot(pkind != PLAN_NONE || (TRACE && tr_cnt))) {
+    if (__ballot(pkind != PLAN_NONE || papplied || (TRACE && tr_cnt))) {
       const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
       if (pkind != PLAN_NONE && m) {
@@ -543,7 +757,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       }
       if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
         uint32_t cc = S.ccount[sgi];
-        uint32_t si = (n.base + n.len - papplied) % A;
+        uint32_t si = (n.base + papply_from) % A;
         for (uint32_t i = 0; i < papplied; ++i, ++cc) {
           if (S.SC) S.stream[(size_t)sgi * S.SC + cc % S.SC] = sar[si].y;
           si = si + 1 == A ? 0 : si + 1;
@@ -621,12 +835,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             if (vals[q - 1] < vals[q]) {
               const int32_t tmp = vals[q]; vals[q] = vals[q - 1]; vals[q - 1] = tmp;
             }
-        int32_t mm = vals[(N + 1) / 2 - 1];
+        int32_t mm = vals[MAJ - 1];
         if (mm > (int32_t)n.len) mm = (int32_t)n.len;
         if (mm > (int32_t)hidx) {
-          cm = mm;
           const uint2 e = sar[(n.base + (uint32_t)mm - 1) % A];
-          ct = e.x; cv = e.y;
+          if (!SPEC || e.x == n.term) {   // SIM_SPEC §8: committed only in the leader's term
+            cm = mm;
+            ct = e.x; cv = e.y;
+          }
         }
       }
       if (__ballot(cm >= 0)) {                       // cluster argmax, lowest id on ties
@@ -755,16 +971,22 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
   out[ci] = h;
 }
 
-template <int N>
-hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+template <int N, bool SPEC>
+void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
   constexpr int CPW = 64 / N;
-  constexpr size_t lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
+  constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = (S.C + CPW - 1) / CPW;
   const uint32_t blocks = (waves + 3) / 4;
   if (S.TC)
-    hipLaunchKernelGGL((tick_kernel<N, true>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
   else
-    hipLaunchKernelGGL((tick_kernel<N, false>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+}
+
+template <int N>
+hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+  if (S.variant & RAFT_VARIANT_SPEC) launch_tick_ns<N, true>(S, t0, nt, st);
+  else launch_tick_ns<N, false>(S, t0, nt, st);
   return hipGetLastError();
 }
 
@@ -782,15 +1004,20 @@ hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st
   }
 }
 
+template <int N, bool TRACE, bool SPEC>
+hipError_t configure_one() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)block_lds_bytes<N, SPEC>());
+}
+
 template <int N>
 hipError_t configure_n() {
-  constexpr int CPW = 64 / N;
-  constexpr int lds = (PW_WORDS + 4 * (CPW * N * N * 8 + LCTR_WORDS)) * sizeof(uint32_t);
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, false>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, true>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipError_t e = hipSuccess;
+  if ((e = configure_one<N, false, false>()) || (e = configure_one<N, true, false>()) ||
+      (e = configure_one<N, false, true>()) || (e = configure_one<N, true, true>()))
+    return e;
+  return hipSuccess;
 }
 
 hipError_t configure_kernels() {

@@ -21,7 +21,7 @@ def random_config(rng):
     n = rng.randint(2, 9)
     cfg = dict(nodes=n, seed=rng.getrandbits(64), log_cap=rng.choice([6, 8, 12]),
                inbox_cap=rng.randint(4, 16), hb=rng.randint(1, 6), el_base=rng.randint(1, 6),
-               el_span=rng.randint(1, 6), variant_flags=int(rng.random() < 0.2),
+               el_span=rng.randint(1, 6), variant_flags=rng.choice([0, 0, 0, 1, 2, 3]),
                commit_stream_cap=rng.choice([0, 2, 16]), trace_cap=rng.choice([0, 2, 64]))
     cfg["trace_entry_cap"] = rng.choice([0, 1, 4096]) if cfg["trace_cap"] else 0
     if rng.random() < 0.5:

@@ -26,6 +26,10 @@ CASES = {
                                  client_ppm=5000, log_cap=64), gid=1, ticks=20000, trace=False),
     "variant_n3": dict(cfg=dict(nodes=3, seed=17, variant_flags=1, client_ppm=150,
                                 drop_ppm=50000, log_cap=64), gid=2, ticks=30000, trace=False),
+    # F4 Spec-Raft control (SIM_SPEC §8) with faults and client traffic, full event trace
+    "spec_n5": dict(cfg=dict(nodes=5, seed=19, variant_flags=2, client_ppm=2000, drop_ppm=100000,
+                             dup_ppm=20000, dmin=1, dmax=30, part_ppm=100000, log_cap=256,
+                             hb=300, el_base=500, el_span=500), gid=4, ticks=30000, trace=True),
 }
 
 

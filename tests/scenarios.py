@@ -443,6 +443,141 @@ def kat_printed_entries(view_of):
         ":type :append-entries, :resp-chan " + CHAN % 0 + "}")
 
 
+# ================================================================ F4 Spec-Raft (SIM_SPEC §8)
+# Not reference behaviour: Raft Figure 2 (Ongaro & Ousterhout 2014), the correct-protocol control.
+SPEC = 2
+
+
+def kat_spec_first_election(view_of):
+    """Voters adopt the candidate's term (Figure 2 "all servers"), keep voted-for, followers
+    become :follower (not :follwer) and the leader keeps voted-for; next = last log index + 1."""
+    nodes = {i: node(deadline=BIG) for i in range(1, 6)}
+    nodes[3] = node(deadline=0)
+    v = view_of(Scenario(5, nodes, variant_flags=SPEC))
+    v.step(1)
+    assert (v.node(3)["role"], v.node(3)["current_term"], v.node(3)["voted_for"]) == \
+        (ROLE["candidate"], 2, 3)
+    v.step(1)
+    for i in (1, 2, 4, 5):
+        r = v.node(i)
+        assert (r["role"], r["current_term"], r["voted_for"]) == (ROLE["follower"], 2, 3), r
+    v.step(2)                                    # t2 first grant, t3 second grant: 3 of 5
+    a = v.node(3)
+    assert (a["role"], a["votes"], a["voted_for"], a["leader_id"]) == (ROLE["leader"], 0, 3, 3)
+    assert a["next_index"] == [1, 1, 0, 1, 1] and a["match_index"] == [0] * 5
+    v.step(1)
+    for i in (1, 2, 4, 5):
+        r = v.node(i)
+        assert (r["role"], r["current_term"], r["voted_for"], r["leader_id"]) == \
+            (ROLE["follower"], 2, 3, 3), r
+    v.step(5)
+    a = v.node(3)
+    assert a["next_index"] == [1, 1, 0, 1, 1] and a["commit_index"] == 0
+    c = v.counters()
+    assert c["leaders"] == 1 and c["ev_vr"] == 4 and c["ev_ar"] == 4 and c["ev_ae"] == 4
+
+
+def kat_spec_replication(view_of):
+    """The whole suffix ships once, the leader commits by majority match, followers learn the
+    commit from the next heartbeat, and nothing is duplicated."""
+    nodes = {1: node("leader", term=2, voted_for=1, leader_id=1, ls={2: (1, 0), 3: (1, 0)},
+                     log=[E1, E2, E3], deadline=0, last_led=2),
+             2: node("follower", term=2, voted_for=1, leader_id=1),
+             3: node("follower", term=2, voted_for=1, leader_id=1)}
+    v = view_of(Scenario(3, nodes, variant_flags=SPEC))
+    v.step(2)                                    # t0 heartbeat, t1 followers append all three
+    assert v.log(2) == [E1, E2, E3] and v.log(3) == [E1, E2, E3]
+    assert v.node(2)["commit_index"] == 0        # leader-commit was 0
+    v.step(1)                                    # t2 reply from 2: match {3, 3, 0} -> commit 3
+    a = v.node(1)
+    assert a["commit_index"] == 3 and v.commit_stream(1) == [10, 20, 30]
+    v.step(1)
+    a = v.node(1)
+    assert a["next_index"] == [0, 4, 4] and a["match_index"] == [0, 3, 3]
+    v.step(3002)                                 # heartbeat at 3003 (hb after t3), lands 3004
+    for i in (2, 3):
+        assert v.log(i) == [E1, E2, E3] and v.node(i)["commit_index"] == 3
+        assert v.commit_stream(i) == [10, 20, 30]
+    c = v.counters()
+    assert c["viol_log"] == 0 and c["entries_appended"] == 6 and c["entries_applied"] == 9
+
+
+F = (3, 40)
+
+
+def kat_spec_truncate_on_conflict(view_of):
+    """A conflicting suffix is truncated at the first term mismatch and replaced; a duplicate or a
+    shorter consistent AppendEntries never shortens the log."""
+    nodes = {1: node("leader", term=3, voted_for=1, leader_id=1, ls={2: (2, 0), 3: (3, 0)},
+                     log=[E1, F], commit=1, deadline=0, last_led=3),
+             2: node("follower", term=3, leader_id=1, log=[E1, (2, 99), (2, 98)], commit=1),
+             3: node("follower", term=3, leader_id=1, log=[E1, F])}
+    q = {(2, 0): [msg("append-entries", 1, term=3, leader_id=1, leader_commit=1,
+                      prev_log_index=1, prev_log_term=E1, entries=[F])],
+         (3, 0): [msg("append-entries", 1, term=3, leader_id=1, leader_commit=1,
+                      prev_log_index=1, prev_log_term=E1, entries=[])]}
+    v = view_of(Scenario(3, nodes, q, variant_flags=SPEC))
+    v.step(1)                                    # t0 heartbeat: prev 1 (E1) + [F] to node 2
+    v.step(1)                                    # t1: the queued duplicates (arrival 1) first
+    assert v.log(2) == [E1, F] and v.node(2)["log_len"] == 2   # (2,99),(2,98) truncated
+    assert v.log(3) == [E1, F]                   # shorter AE: log kept
+    v.step(1)                                    # t2: the heartbeat's copies: idempotent
+    assert v.log(2) == [E1, F] and v.log(3) == [E1, F]
+    assert v.node(2)["commit_index"] == 1 and v.node(2)["fault"] == 0
+
+
+def kat_spec_commit_rule(view_of):
+    """Figure 8: a majority-replicated entry of an older term is not committed by counting; an
+    entry of the leader's own term commits it indirectly."""
+    nodes = {1: node("leader", term=4, voted_for=1, leader_id=1, ls={2: (3, 0), 3: (3, 0)},
+                     log=[(2, 10), (2, 20)], last_led=4),
+             2: node("follower", term=4, leader_id=1, log=[(2, 10), (2, 20)]), 3: node(term=4)}
+    q = {(1, 1): [msg("append-response", 0, term=4, id=2, success=True, commit=0, log_index=2),
+                  msg("append-response", 2, term=4, id=2, success=True, commit=0, log_index=3)],
+         (1, 0): [msg("client-set", 1, command=77)]}
+    v = view_of(Scenario(3, nodes, q, variant_flags=SPEC))
+    v.step(1)
+    assert v.node(1)["commit_index"] == 0 and v.node(1)["match_index"] == [0, 2, 0]
+    v.step(1)
+    assert v.log(1) == [(2, 10), (2, 20), (4, 77)]
+    v.step(1)
+    a = v.node(1)
+    assert a["commit_index"] == 3 and v.commit_stream(1) == [10, 20, 77]
+    assert a["next_index"][1] == 4 and a["match_index"][1] == 3
+
+
+def kat_spec_vote_rules(view_of):
+    """Up-to-date check (last term, then length), one vote per term, term update on any RPC."""
+    def rv(term, cand, idx, last):
+        return msg("request-vote", 0, term=term, candidate_id=cand, last_log_index=idx,
+                   last_log_term=last)
+    for flags in (SPEC, SPEC | 1):
+        nodes = {1: node(term=3, log=[(3, 1)]), 2: node(term=3), 3: node(term=3)}
+        q = {(1, 0): [rv(3, 2, 5, (2, 9)), rv(3, 2, 0, None), rv(3, 3, 1, (3, 5)),
+                      rv(3, 2, 9, (4, 0)), rv(3, 3, 1, (3, 5)), rv(5, 2, 0, None)]}
+        v = view_of(Scenario(3, nodes, q, variant_flags=flags))
+        v.step(1)                                # older last term: refused (granted without check)
+        assert v.node(1)["voted_for"] == (0 if flags == SPEC else 2)
+        if flags != SPEC:
+            continue
+        v.step(1)
+        assert v.node(1)["voted_for"] == 0       # empty log is behind
+        v.step(1)
+        assert v.node(1)["voted_for"] == 3       # same last term, index >= 1: granted
+        v.step(1)
+        assert v.node(1)["voted_for"] == 3       # one vote per term
+        v.step(1)
+        assert v.node(1)["voted_for"] == 3       # the same candidate again
+        v.step(1)
+        r = v.node(1)
+        assert (r["current_term"], r["voted_for"], r["role"]) == (5, 0, ROLE["follower"])
+        assert r["fault"] == 0
+
+
+SPEC_ALL = [kat_spec_first_election, kat_spec_replication, kat_spec_truncate_on_conflict,
+            kat_spec_commit_rule, kat_spec_vote_rules]
+
 ALL = [kat_majority, kat_first_election, kat_duplication, kat_truncate_crash, kat_cce, kat_npe,
        kat_partial_leader_state, kat_stale_step_down, kat_two_leaders_one_term, kat_vote_rules,
-       kat_variant_no_log_check, kat_client_set, kat_printed_trace, kat_printed_entries]
+       kat_variant_no_log_check, kat_client_set, kat_printed_trace, kat_printed_entries,
+       *SPEC_ALL]

@@ -47,6 +47,18 @@ CASES = {
                          arena_cap=32, dup_ppm=100000, dmax=10, trace_cap=16, trace_entry_cap=64),
     "fast_timers": dict(n_clusters=1000, nodes=5, seed=29, hb=30, el_base=50, el_span=50,
                         client_ppm=20000, log_cap=128, **FAULTS),
+    # F4 Spec-Raft control (SIM_SPEC §8) and its bug-injected form
+    "spec_c3": dict(n_clusters=2048, nodes=5, seed=41, client_ppm=2000, log_cap=256,
+                    variant_flags=2, commit_stream_cap=64, **FAULTS),
+    "spec_nolog": dict(n_clusters=1024, nodes=5, seed=43, client_ppm=5000, log_cap=512, hb=300,
+                       el_base=500, el_span=500, variant_flags=3, **FAULTS),
+    "spec_n9": dict(n_clusters=512, nodes=9, seed=45, client_ppm=3000, log_cap=1024,
+                    variant_flags=2, commit_stream_cap=256, dup_ppm=20000, dmax=8),
+    "spec_n4_traced": dict(n_clusters=512, nodes=4, seed=47, client_ppm=4000, log_cap=128,
+                           variant_flags=2, trace_cap=32, trace_entry_cap=256, **FAULTS),
+    "spec_tight": dict(n_clusters=512, nodes=3, seed=49, client_ppm=30000, log_cap=24,
+                       arena_cap=48, hb=40, el_base=60, el_span=60, variant_flags=2,
+                       inbox_cap=3, **FAULTS),
 }
 
 
@@ -103,6 +115,26 @@ def test_gpu_printed_trace_matches_oracle():
             assert tg == r.edn_trace(c, i), (c, i)
             n_entries += tg.count(":val ")
     assert n_entries > 0
+
+
+def test_gpu_spec_raft_safety_at_scale():
+    """BASELINE config 5 shape on the GPU: 65,536 Spec-Raft clusters with faults, client traffic
+    and fast timers show no violation (control), while the same clusters with the up-to-date vote
+    check dropped do; both bit-exact against the oracle on a sampled slice."""
+    base = dict(n_clusters=65536, nodes=5, seed=51, client_ppm=5000, log_cap=256, hb=300,
+                el_base=500, el_span=500, **FAULTS)
+    ctl, bug = helpers.gpu(variant_flags=2, **base), helpers.gpu(variant_flags=3, **base)
+    for s in (ctl, bug):
+        s.step(20000)
+    c, b = ctl.counters(), bug.counters()
+    assert c["leaders"] > 100000 and c["viol_election"] == c["viol_log"] == c["viol_complete"] == 0
+    assert b["viol_complete"] > 0 and b["first_violation_tick"] is not None
+    lo = 4096
+    for flags, sim in ((2, ctl), (3, bug)):
+        r = helpers.oracle(**dict(base, n_clusters=lo, variant_flags=flags))
+        helpers.oracle_threads(r, helpers.cpu_threads())
+        r.step(20000)
+        assert np.array_equal(sim.digest(0, lo), r.digest())
 
 
 def test_gpu_shard_invariance():

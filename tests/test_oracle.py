@@ -71,6 +71,51 @@ def test_oracle_equals_python_restatement(seed):
     assert c["first_violation_tick"] == pc.first_violation
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_spec_oracle_equals_python_restatement(seed):
+    """F4 Spec-Raft (flag 2) and its bug-injected form (flags 3), same cross-check."""
+    rng = random.Random(7000 + seed)
+    cfg = random_config(rng)
+    cfg["variant_flags"] = rng.choice([2, 3])
+    gid = rng.randrange(1 << 20)
+    be = helpers.oracle(n_clusters=1, cluster_offset=gid, **cfg)
+    pc = pyref.PyCluster(helpers.py_config(**cfg), gid)
+    for t in range(6000):
+        pc.step(t)
+    be.step(6000)
+    c = be.counters()
+    if c["payload_evicted"]:
+        pytest.skip("arena eviction: the Python restatement models ideal snapshots")
+    helpers.compare_py_backend(pc, be, 0)
+    for k, v in pc.cnt.items():
+        assert c[k] == v, (k, c[k], v)
+    assert c["first_violation_tick"] == pc.first_violation
+
+
+FAULTS = dict(drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
+
+
+@pytest.mark.parametrize("nodes", [3, 4, 5, 7])
+def test_spec_raft_is_safe_and_the_injected_bug_is_not(nodes):
+    """BASELINE config 5 on the CPU: the Spec-Raft control (SIM_SPEC §8) shows no violation of
+    election safety, log matching or leader completeness under drop/dup/delay/partitions with
+    client traffic and fast timers, while dropping only the up-to-date vote check (flags 3) lets a
+    stale candidate win and lose committed entries (leader completeness)."""
+    base = dict(n_clusters=512, nodes=nodes, seed=5, client_ppm=10000, log_cap=512, hb=300,
+                el_base=500, el_span=500, **FAULTS)
+    ctl = helpers.oracle(variant_flags=2, **base)
+    bug = helpers.oracle(variant_flags=3, **base)
+    for be in (ctl, bug):
+        helpers.oracle_threads(be, helpers.cpu_threads())
+        be.step(30000)
+    c, b = ctl.counters(), bug.counters()
+    assert c["leaders"] > 1000 and c["entries_applied"] > 10000
+    assert c["viol_election"] == c["viol_log"] == c["viol_complete"] == 0
+    assert c["first_violation_tick"] is None
+    assert b["viol_complete"] > 0 and b["viol_election"] == 0
+    assert b["first_violation_tick"] is not None
+
+
 def test_message_conservation():
     """sent + client_injected - dropped - partitioned + duplicated = delivered + overflow + to_halted."""
     be = helpers.oracle(n_clusters=64, nodes=5, seed=5, drop_ppm=100000, dup_ppm=50000, dmax=20,
