@@ -27,11 +27,19 @@ __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t
   return fnv(h, fault);
 }
 
-// P2 fault draws for one emitted message, written into the (sender, receiver) LDS cell.
+// One emitted message a = (hdr, term, a, b), b = (eterm, eval, poff, -) into its (sender,
+// receiver) LDS cell; transmit() adds the delivery pack as the cell's last word.
+__device__ __forceinline__ void cell_put(uint32_t* cl, uint4 a, uint4 b) {
+  reinterpret_cast<uint4*>(cl)[0] = a;
+  reinterpret_cast<uint4*>(cl)[1] = b;
+}
+
+// P2 fault draws for one emitted message whose words are already in cell `cl`: the delivery pack
+// (copy delays and count) goes to the cell's last word and the receiver's bit into sentmask.
 template <int N>
 __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
                                          uint32_t p, bool part, uint32_t sides, uint32_t* cl,
-                                         uint4 a, uint4 b, uint32_t& sentmask, uint32_t* lctr) {
+                                         uint32_t& sentmask, uint32_t* lctr) {
   lctr_add(lctr, RAFT_CTR_SENT, 1);
   if (part && (((sides >> id) ^ (sides >> p)) & 1)) {
     lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
@@ -53,9 +61,7 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
       pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
     }
   }
-  b.w = pack;
-  reinterpret_cast<uint4*>(cl)[0] = a;
-  reinterpret_cast<uint4*>(cl)[1] = b;
+  cl[7] = pack;
   sentmask |= 1u << p;
 }
 
@@ -82,6 +88,44 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   uint4* rec = reinterpret_cast<uint4*>(S.tr + ((size_t)gi * S.TC + seq % S.TC) * 32);
 #pragma unroll
   for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Copy `cnt` arena entries from slot si of `src` to slot di of `dst` (slots wrap at A), eight per
+// batch: a batch's loads are all issued before its stores, so a long copy pays one memory round
+// trip per eight entries rather than one per entry. Ascending order with every load of a batch
+// ahead of its stores keeps an overlapping relocation (dst ahead of src by d < A) exact: a slot
+// is only overwritten after it has been read, as in the oracle's element-by-element copy.
+#ifndef RS_COPY_BATCH
+#define RS_COPY_BATCH 4
+#endif
+__device__ __forceinline__ void arena_copy(uint2* dst, uint32_t di, const uint2* src, uint32_t si,
+                                           uint32_t cnt, uint32_t A) {
+  constexpr uint32_t B = RS_COPY_BATCH;
+  uint32_t i = 0;
+  if (A >= B) {
+    for (; i + B <= cnt; i += B) {
+      uint2 v[B];
+#pragma unroll
+      for (int j = 0; j < (int)B; ++j) {
+        const uint32_t s = si + j;
+        v[j] = src[s >= A ? s - A : s];
+      }
+#pragma unroll
+      for (int j = 0; j < (int)B; ++j) {
+        const uint32_t d = di + j;
+        dst[d >= A ? d - A : d] = v[j];
+      }
+      si += B;
+      si = si >= A ? si - A : si;
+      di += B;
+      di = di >= A ? di - A : di;
+    }
+  }
+  for (; i < cnt; ++i) {
+    dst[di] = src[si];
+    si = si + 1 == A ? 0 : si + 1;
+    di = di + 1 == A ? 0 : di + 1;
+  }
 }
 
 // F4 Spec-Raft control (SIM_SPEC §8): one event of a running node under Raft's Figure 2 rules.
@@ -255,11 +299,14 @@ __device__ __forceinline__ void spec_handle(
   }
 }
 
-// LDS words per wave: message cells [cluster][sender][receiver], counters, and (Spec-Raft) the
-// wave's pre-tick arena frontiers.
+// LDS words per wave: message cells [cluster][sender][receiver other than the sender] of 8
+// words, counters, and (Spec-Raft) the wave's pre-tick arena frontiers.
+constexpr int CELLW = 8;
+template <int N>
+constexpr int cell_words() { return (64 / N) * N * (N - 1) * CELLW; }
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
-  return (64 / N) * N * N * 8 + LCTR_WORDS + (SPEC ? 64 : 0);
+  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0);
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -268,10 +315,13 @@ constexpr size_t block_lds_bytes() {
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
 // faithful kernel carries none of its code.
+#ifndef RS_MIN_WAVES_PER_EU
+#define RS_MIN_WAVES_PER_EU 1
+#endif
 template <int N, bool TRACE, bool SPEC>
-__global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
+tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
-  constexpr int CELL_WORDS = CPW * N * N * 8;
   constexpr int WAVE_WORDS = wave_lds_words<N, SPEC>();
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
@@ -282,7 +332,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   if (threadIdx.x < 32) pw[threadIdx.x] = S.client_pw[threadIdx.x];
   __syncthreads();
   uint32_t* cells = smem + PW_WORDS + wv * WAVE_WORDS;
-  uint32_t* lctr = cells + CELL_WORDS;
+  uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
@@ -294,7 +344,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
   const uint32_t g = S.goff + c;
   const int bl = (cs < CPW ? cs : 0) * N;
   const uint32_t NN = S.NN, A = S.A;
-  uint32_t* mycells = cells + (cs < CPW ? cs : 0) * N * N * 8;
+  uint32_t* mycells = cells + (cs < CPW ? cs : 0) * N * (N - 1) * CELLW;
 
   NodeR n = {};
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
@@ -649,14 +699,22 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             sides = pw.y;
           }
           if (emit == 3) {
-            transmit<N>(S, sg, t, id, src, part, sides, mycells + ((k * N) + src - 1) * 8, ra, rb,
-                        sentmask, lctr);
+            uint32_t* cl =
+                mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
+            cell_put(cl, ra, rb);
+            transmit<N>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
           } else {
+            // Message words first, for every peer at once: the next-index loads (and then the
+            // prev-entry loads) of all peers are independent, so they overlap instead of paying
+            // one memory round trip per peer; the fault draws follow in a compact loop.
+            int32_t nxs[N];
+#pragma unroll
+            for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? S.next[p * NN + sgi] : 0;
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
               if (SPEC && emit == 2) {                    // SIM_SPEC §8 broadcast
-                const int32_t pv = S.next[(p - 1) * NN + sgi] - 1;
+                const int32_t pv = nxs[p - 1] - 1;
                 const uint32_t prev = pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
                 uint32_t ep = 0, et = 0, evl = 0;
                 if (prev) {
@@ -668,7 +726,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
                                 n.commit, prev);
                 rb = make_uint4(et, evl, pc ? n.base + prev : 0, 0);
               } else if (emit == 2) {
-                const int32_t nx = S.next[(p - 1) * NN + sgi];
+                const int32_t nx = nxs[p - 1];
                 const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
                 const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
                 uint32_t ep = 0, et = 0, evl = 0, pc = 0, po = 0;
@@ -682,8 +740,14 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
                                 n.commit, (uint32_t)prev);
                 rb = make_uint4(et, evl, po, 0);
               }
-              transmit<N>(S, sg, t, id, p, part, sides, mycells + ((k * N) + p - 1) * 8, ra, rb,
-                          sentmask, lctr);
+              cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
+            }
+#pragma unroll 1
+            for (int p = 1; p <= N; ++p) {
+              if (p == (int)id) continue;
+              transmit<N>(S, sg, t, id, p, part, sides,
+                          mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, sentmask,
+                          lctr);
             }
           }
         }
@@ -704,7 +768,8 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       uint32_t copy = 0;
       while (inmask) {
         const int s = __builtin_ctz(inmask);
-        const uint4* cl = reinterpret_cast<const uint4*>(mycells + (s * N + k) * 8);
+        const uint4* cl =
+            reinterpret_cast<const uint4*>(mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
         const uint4 a = cl[0], b = cl[1];
         const uint32_t d = copy == 0 ? (b.w & 0xFF) : ((b.w >> 8) & 0xFF);
         const int which = (a.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
@@ -726,14 +791,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
       if (pkind != PLAN_NONE && m) {
         // physical slots advance with a wrap instead of a per-entry modulo
-        if (preloc) {
-          uint32_t si = pold_base % A, di = n.base % A;
-          for (uint32_t i = 0; i < pold_len; ++i) {
-            sar[di] = sar[si];
-            si = si + 1 == A ? 0 : si + 1;
-            di = di + 1 == A ? 0 : di + 1;
-          }
-        }
+        if (preloc) arena_copy(sar, n.base % A, sar, pold_base % A, pold_len, A);
         uint32_t di = (n.base + pold_len) % A;
         if (pkind == PLAN_ENTRY) {
           sar[di] = make_uint2(pet, pev);
@@ -747,11 +805,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
             sar[di] = make_uint2(0, 0);
             di = di + 1 == A ? 0 : di + 1;
           }
-          for (uint32_t i = evicted; i < m; ++i) {
-            sar[di] = sa[si];
-            si = si + 1 == A ? 0 : si + 1;
-            di = di + 1 == A ? 0 : di + 1;
-          }
+          arena_copy(sar, di, sa, si, m - evicted, A);
           lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
         }
       }
@@ -779,8 +833,9 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
     }
 
     // ---------------------------------------------------------------- P4 invariant checker
-    if (__ballot(elected || appended_at >= 0 || mchg)) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    // the majority-match scan can raise hwm only when the leader's log reaches past it
+    const bool mcheck = (elected || mchg) && n.len > hidx;
+    if (__ballot(elected || appended_at >= 0 || mcheck)) {
       if (__ballot(elected)) {                       // election safety
         bool bad = false;
 #pragma unroll
@@ -791,6 +846,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
         if (bad) violation(lctr, RAFT_CTR_VIOL_ELECTION, t);
       }
       if (__ballot(appended_at >= 0)) {              // log matching
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
         bool bad = false;
 #pragma unroll
         for (int s = 0; s < N; ++s) {
@@ -819,7 +875,7 @@ __global__ void __launch_bounds__(256) tick_kernel(DevSim S, uint32_t t0, uint32
       }
       int32_t cm = -1;
       uint32_t ct = 0, cv = 0;
-      if (active && n.role == RAFT_LEADER && (elected || mchg)) {
+      if (active && n.role == RAFT_LEADER && mcheck) {
         int32_t vals[N];
         vals[0] = (int32_t)n.len;
         int j = 1;

@@ -1,0 +1,45 @@
+"""A/B kernel builds in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+Usage: python scripts/ab_probe.py LIB_A LIB_B ... ; prints the median and min kernel ms per
+10k-tick launch for each build on each workload, and whether the builds agree on the state."""
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "raft-simulation_amd")]
+from raftsim._backend import Backend  # noqa: E402
+
+FAULTS = dict(drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
+WORK = {
+    "c2": dict(n_clusters=65536, nodes=5, seed=42),
+    "c3": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=10000, log_cap=256, **FAULTS),
+    "c4_n9": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=250000, log_cap=4096),
+}
+
+
+def main():
+    libs = [a for a in sys.argv[1:] if not a.startswith("--")]
+    only = [a[2:] for a in sys.argv[1:] if a.startswith("--")]
+    rounds = 5
+    for wname, cfg in WORK.items():
+        if only and wname not in only:
+            continue
+        sims = [Backend(lib, "raft_sim_", **cfg) for lib in libs]
+        for s in sims:
+            s.step(10000)                               # warm up to a steady state
+        times = [[] for _ in libs]
+        for _ in range(rounds):
+            for i, s in enumerate(sims):
+                s.step(10000)
+                times[i].append(s.last_step_timing()[0])
+        digests = {bytes(s.digest(0, 256)) for s in sims}
+        for lib, ts in zip(libs, times):
+            print(f"{wname:6s} {Path(lib).name:28s} median {statistics.median(ts):8.3f} ms  "
+                  f"min {min(ts):8.3f} ms", flush=True)
+        print(f"{wname:6s} builds agree on state: {len(digests) == 1}", flush=True)
+        for s in sims:
+            s.close()
+
+
+if __name__ == "__main__":
+    main()
