@@ -135,6 +135,14 @@ def main():
         ticks_per_launch = args.steps * TICKS_PER_STEP / max(1, launches)
         node_ticks_per_launch = args.clusters * NODES * ticks_per_launch
         achieved = bpnt * node_ticks_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        # The fused kernel's own minimum HBM traffic per launch: hot node state in and out once
+        # (S_node(N) = 32 + 8N bytes each way), plus every message written to and read from a
+        # queue (64 B) and every log entry copied (16 B) -- what a perfect implementation of THIS
+        # design must move; compare with `traffic` (PMC) and with the peak.
+        launch_share = node_ticks_per_launch / max(1, total_node_ticks)
+        fused_bytes = (2 * (32 + 8 * NODES) * args.clusters
+                       + (64 * delta["delivered"] + 16 * delta["entries_appended"]) * launch_share)
+        fused_gbs = fused_bytes / (avg_launch_ms * 1e-3) / 1e9
         value = total_node_ticks / elapsed_max
         out = {
             "metric": "simulated node-ticks/sec (5-node Raft)",
@@ -159,7 +167,9 @@ def main():
                          "traffic": load_traffic(),
                          "algorithmic_bytes_per_node_tick": bpnt,
                          "msgs_per_node_tick": m, "entries_per_node_tick": e,
-                         "avg_launch_ms": avg_launch_ms, "ticks_per_launch": ticks_per_launch},
+                         "avg_launch_ms": avg_launch_ms, "ticks_per_launch": ticks_per_launch,
+                         "fused_model": {"bytes_per_launch": fused_bytes, "achieved": fused_gbs,
+                                         "frac": fused_gbs / HBM_PEAK_GBS}},
             "counters": {k: v for k, v in delta.items() if v and k != "first_violation_tick"},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -33,7 +33,7 @@ durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
 fetch, write = avg.get("FETCH_SIZE", 0) * 1024, avg.get("WRITE_SIZE", 0) * 1024
 out = {"tag": tag, "kernel": "rs::tick_kernel<5>", "launches_profiled": len(durs),
        "avg_duration_ns": sum(durs) / max(1, len(durs)),
-       "vgpr": trace[0].get("VGPR_Count") if trace else None,
+       "vgpr": next((r.get("VGPR_Count") for r in trace if "tick_kernel" in r["Kernel_Name"]), None),
        "pmc_per_launch": avg,
        "hbm_fetch_bytes_raw": fetch, "hbm_write_bytes": write,
        "hbm_bytes_per_launch": 2 * fetch + write,
