@@ -49,6 +49,14 @@ enum raft_variant {
   RAFT_VARIANT_SPEC = 2               /* F4 Spec-Raft control: Raft Figure 2 rules (SIM_SPEC §8) */
 };
 
+/* How clusters are packed onto waves before each launch. Clusters are independent and Philox is
+ * keyed by the global cluster id, so every packing gives bit-identical results; it only decides
+ * which clusters share a wave, i.e. how many of a wave's ticks are active. */
+enum raft_schedule {
+  RAFT_SCHED_ALIGNED = 0, /* regroup clusters by their next event tick before every launch */
+  RAFT_SCHED_FIXED = 1    /* cluster c always on wave c / floor(64/N) */
+};
+
 /* Replaces `-main`'s argv (core.clj:197-200), the hard-coded timeouts (core.clj:173-174) and the
  * chan buffer sizes (server.clj:37, client.clj:18). Defaults: raft_sim_default_config(). */
 typedef struct raft_sim_config {
@@ -69,7 +77,7 @@ typedef struct raft_sim_config {
   uint32_t commit_stream_cap; /* per-node ring of committed :val's (log.clj:69-76); 0 = off */
   uint32_t trace_cap;         /* per-node ring of `wait` events (core.clj:182-186); 0 = off */
   uint32_t trace_entry_cap;   /* per-node ring of the :entries those events carried */
-  uint32_t reserved[1];
+  uint32_t schedule;          /* cluster->wave packing, enum raft_schedule (results identical) */
 } raft_sim_config_t;
 
 /* Canonical node record: the node map of init-node (core.clj:31-38) plus the log atom

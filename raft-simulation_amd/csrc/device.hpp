@@ -45,6 +45,7 @@ struct DevSim {
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)
+  const uint32_t* perm;     // [C] wave slot -> cluster (RAFT_SCHED_ALIGNED), null = identity
 };
 
 // Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).
@@ -182,25 +183,6 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
   q.c += 1;
   if (pos == 0) q.arr = arr;
   lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-}
-
-// Take the head of queue `which`.
-__device__ __forceinline__ void qpop(const DevSim& S, uint32_t gi, int which, QueueR& q, uint4& m0,
-                                     uint4& m1) {
-  uint32_t* qb = qslots(S, gi, which);
-  const uint32_t head = q.h;
-  const uint4* sp = reinterpret_cast<const uint4*>(qb + head * 8);
-  m0 = sp[0];
-  m1 = sp[1];
-  const uint32_t nh = wrapq(head + 1, S.Q);
-  q.h = nh;
-  q.c -= 1;
-  if (q.c) {
-    q.arr = qb[nh * 8];
-  } else {
-    q.arr = INF;
-    q.tail = 0;
-  }
 }
 
 }  // namespace rs

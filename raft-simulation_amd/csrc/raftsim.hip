@@ -6,10 +6,14 @@
 #include <algorithm>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "device.hpp"
 
 namespace rs {
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st);
+hipError_t launch_sched_key(const DevSim& S, uint32_t t0, uint32_t* keys, uint32_t* ids,
+                            hipStream_t st);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -43,6 +47,10 @@ struct raft_sim {
   double last_ms;
   uint32_t last_launches;
   unsigned long long* client_pw;
+  // RAFT_SCHED_ALIGNED: per-launch (next-event key, cluster) pairs, sorted into d.perm
+  uint32_t *sk_in, *sk_out, *sid_in, *sid_out;
+  void* sort_tmp;
+  size_t sort_tmp_bytes;
 };
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -74,6 +82,7 @@ static int validate_cfg(const raft_sim_config_t* c) {
       c->client_ppm > 1000000)
     return fail(-EINVAL, "ppm values must be <= 1e6");
   if (c->variant_flags & ~3u) return fail(-EINVAL, "variant_flags: only bits 0-1 are defined");
+  if (c->schedule > RAFT_SCHED_FIXED) return fail(-EINVAL, "schedule: 0 (aligned) or 1 (fixed)");
   if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
     return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
   return 0;
@@ -158,6 +167,21 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
     return rc;
   }
   d.client_pw = s->client_pw;
+  if (cfg->schedule == RAFT_SCHED_ALIGNED) {
+    if ((rc = dalloc(s, &s->sk_in, s->C)) || (rc = dalloc(s, &s->sk_out, s->C)) ||
+        (rc = dalloc(s, &s->sid_in, s->C)) || (rc = dalloc(s, &s->sid_out, s->C))) {
+      raft_sim_destroy(s);
+      return rc;
+    }
+    size_t bytes = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->sk_in, s->sk_out, s->sid_in,
+                                           s->sid_out, (int)s->C, 0, 16) != hipSuccess ||
+        (rc = dalloc(s, reinterpret_cast<uint8_t**>(&s->sort_tmp), bytes))) {
+      raft_sim_destroy(s);
+      return rc ? rc : fail(-EIO, "hipcub radix-sort sizing failed");
+    }
+    s->sort_tmp_bytes = bytes;
+  }
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreate(&s->ev_start)) != hipSuccess ||
@@ -193,7 +217,16 @@ int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
   HIP_OK(hipEventRecord(s->ev_start, s->stream));
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
-    HIP_OK(rs::launch_tick(s->d, (uint32_t)s->tick + done, nt, s->stream));
+    const uint32_t t0 = (uint32_t)s->tick + done;
+    if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
+      // pack clusters with the same next event onto the same waves for this launch
+      HIP_OK(rs::launch_sched_key(s->d, t0, s->sk_in, s->sid_in, s->stream));
+      HIP_OK(hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, s->sort_tmp_bytes, s->sk_in,
+                                                s->sk_out, s->sid_in, s->sid_out, (int)s->C, 0,
+                                                16, s->stream));
+      s->d.perm = s->sid_out;
+    }
+    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
     done += nt;
     ++launches;
   }

@@ -27,11 +27,20 @@ __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t
   return fnv(h, fault);
 }
 
-// One emitted message a = (hdr, term, a, b), b = (eterm, eval, poff, -) into its (sender,
-// receiver) LDS cell; transmit() adds the delivery pack as the cell's last word.
+// LDS message cells. A node emits either one broadcast or one reply per tick, and the words
+// (term, a) of a broadcast are the same for every peer, so they live once per sender in a 2-word
+// sender record; each (sender, receiver) pair cell holds the other six: hdr, b, eterm, eval, poff
+// and the delivery pack transmit() adds. 26 words per five-node sender instead of 32 keeps a
+// block of four waves under 1/6 of the CU's LDS.
+constexpr int CELLW = 6;
+constexpr int SRECW = 2;
+
+// One emitted message a = (hdr, term, a, b), b = (eterm, eval, poff, -) into its pair cell (the
+// sender record is written once per emission by the caller).
 __device__ __forceinline__ void cell_put(uint32_t* cl, uint4 a, uint4 b) {
-  reinterpret_cast<uint4*>(cl)[0] = a;
-  reinterpret_cast<uint4*>(cl)[1] = b;
+  reinterpret_cast<uint2*>(cl)[0] = make_uint2(a.x, a.w);
+  reinterpret_cast<uint2*>(cl)[1] = make_uint2(b.x, b.y);
+  cl[4] = b.z;
 }
 
 // P2 fault draws for one emitted message whose words are already in cell `cl`: the delivery pack
@@ -61,7 +70,7 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
       pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
     }
   }
-  cl[7] = pack;
+  cl[CELLW - 1] = pack;
   sentmask |= 1u << p;
 }
 
@@ -138,8 +147,7 @@ __device__ __forceinline__ void spec_handle(
     uint32_t id, int k, int bl, uint32_t sgi, uint32_t peers, uint4 m0, uint4 m1,
     uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
     uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
-    uint32_t& pold_base, uint32_t& pold_len, uint32_t& preloc, uint32_t& pet, uint32_t& pev,
-    uint32_t& papplied, uint32_t& papply_from, int& appended_at, bool& elected, bool& mchg) {
+    uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg) {
   const uint32_t A = S.A, NN = S.NN;
   if (which < 0) {
     if (n.role == RAFT_LEADER) {                                  // heartbeat
@@ -213,21 +221,20 @@ __device__ __forceinline__ void spec_handle(
       const uint32_t mc = mb + pcnt - kk;
       if (mc) {                               // truncate at kk, append payload [kk - b, pcnt)
         pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff + (kk - mb); ppcnt = mc;
-        pold_base = n.base; pold_len = kk;
+        pold_base = n.base;
         if (kk < n.len || n.base + n.len != n.front) {
           preloc = 1;
           n.base = n.front;
           n.front += kk;
         }
         n.front += mc;
-        appended_at = (int)kk;
         n.len = mb + pcnt;
         appended = mc;
       }
       if (ma > n.commit) {
         const uint32_t nc = ma < mb + pcnt ? ma : mb + pcnt;
         if (nc > n.commit) {
-          applied = nc - n.commit; papplied = applied; papply_from = n.commit;
+          applied = nc - n.commit; papplied = applied;
           n.commit = nc;
         }
       }
@@ -236,15 +243,14 @@ __device__ __forceinline__ void spec_handle(
     }
     case RAFT_MSG_CLIENT_SET: {                                   // as client-set-handler 151-160
       if (n.role != RAFT_LEADER) break;
-      pkind = PLAN_ENTRY; pet = n.term; pev = ma;
-      pold_base = n.base; pold_len = n.len;
+      pkind = PLAN_ENTRY; ppoff = n.term; ppcnt = ma;
+      pold_base = n.base;
       if (n.base + n.len != n.front) {
         preloc = 1;
         n.base = n.front;
         n.front += n.len;
       }
       n.front += 1;
-      appended_at = (int)n.len;
       n.len += 1;
       n.seq = 0;
       appended = 1;
@@ -289,7 +295,7 @@ __device__ __forceinline__ void spec_handle(
       int32_t mm = vals[MAJ - 1];
       if (mm > (int32_t)n.len) mm = (int32_t)n.len;
       if (mm > (int32_t)n.commit && sar[(n.base + (uint32_t)mm - 1) % A].x == n.term) {
-        applied = (uint32_t)mm - n.commit; papplied = applied; papply_from = n.commit;
+        applied = (uint32_t)mm - n.commit; papplied = applied;
         n.commit = (uint32_t)mm;
       }
       break;
@@ -299,11 +305,13 @@ __device__ __forceinline__ void spec_handle(
   }
 }
 
-// LDS words per wave: message cells [cluster][sender][receiver other than the sender] of 8
-// words, counters, and (Spec-Raft) the wave's pre-tick arena frontiers.
-constexpr int CELLW = 8;
+// LDS words per wave: pair cells [cluster][sender][receiver other than the sender] of CELLW
+// words, then sender records [cluster][sender] of SRECW words, counters, and (Spec-Raft) the
+// wave's pre-tick arena frontiers.
 template <int N>
-constexpr int cell_words() { return (64 / N) * N * (N - 1) * CELLW; }
+constexpr int pair_words() { return (64 / N) * N * (N - 1) * CELLW; }
+template <int N>
+constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0);
@@ -337,14 +345,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
   const uint32_t wave = blockIdx.x * 4 + wv;
-  const int cs = lane / N, k = lane - cs * N;
-  const uint32_t c = wave * CPW + cs;
-  const bool active = lane < CPW * N && c < S.C;
-  const uint32_t gi = c * N + k, id = k + 1, peers = ALL & ~(1u << id);
+  const int cs = lane / N, k0 = lane - cs * N;
+  const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
+  const bool active = lane < CPW * N && slot < S.C;
+  const uint32_t c = active && S.perm ? S.perm[slot] : slot;
+  const uint32_t gi = c * N + k0;
   const uint32_t g = S.goff + c;
-  const int bl = (cs < CPW ? cs : 0) * N;
+  const int bl0 = (cs < CPW ? cs : 0) * N;     // the cluster's first lane
   const uint32_t NN = S.NN, A = S.A;
-  uint32_t* mycells = cells + (cs < CPW ? cs : 0) * N * (N - 1) * CELLW;
 
   NodeR n = {};
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
@@ -380,10 +388,16 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
     const bool live = active && !n.fault;
-    // Opaque per-tick copy of the node index: keeps the compiler from hoisting every address
-    // the event path might use out of the tick loop (that costs ~30 loop-carried VGPRs).
+    // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
+    // address and shuffle index the active-tick phases use out of the tick loop, where each would
+    // hold a VGPR across all ticks (~50 VGPRs in all); recomputing them costs a few VALU per
+    // active tick.
     uint32_t sgi = gi, sg = g;
-    asm volatile("" : "+v"(sgi), "+v"(sg));
+    int k = k0, bl = bl0;
+    asm volatile("" : "+v"(sgi), "+v"(sg), "+v"(k), "+v"(bl));
+    const uint32_t id = k + 1, peers = ALL & ~(1u << id);
+    uint32_t* const mycells = cells + bl * (N - 1) * CELLW;
+    uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
     uint2* const sar = arena_of(S, sgi);
     if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
       fr[lane] = n.front;
@@ -423,9 +437,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     const bool req_ok = live && (dcs || n.rq.arr <= t);
     const bool res_ok = live && n.rs.arr <= t;
     uint32_t sentmask = 0;
-    uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, pold_len = 0,
-             preloc = 0, pet = 0, pev = 0, papplied = 0, papply_from = 0;
-    int appended_at = -1;
+    // P3 plan: PAYLOAD copies ppcnt entries from psrc's arena slot ppoff, ENTRY appends the
+    // entry (ppoff, ppcnt) = (term, val); the old log starts at pold_base and (preloc) is first
+    // moved to the node's new base. The old length (n.len - entries added) and the first applied
+    // position (n.commit - papplied) are derived in P3 rather than held across P2.
+    uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, preloc = 0,
+             papplied = 0;
     bool elected = false, mchg = false;
     uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
     if (live && (req_ok || res_ok || t >= n.deadline)) {
@@ -454,10 +471,28 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
       }
       if (which >= 0 && !(dcs && which == 0)) {
-        QueueR q = which ? n.rs : n.rq;
-        qpop(S, sgi, which, q, m0, m1);
-        if (which) n.rs = q;
-        else n.rq = q;
+        // Take the queue head (qpop): both loads are issued first, and a non-leader's EVENT draw
+        // (needed for its next timeout whatever the message does, unless it becomes leader) is
+        // computed in their shadow. The next head's arrival is loaded unconditionally (a slot of
+        // the ring is always in bounds) and used only when the queue stays non-empty.
+        const QueueR q = which ? n.rs : n.rq;
+        const uint32_t* qb = qslots(S, sgi, which);
+        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * 8);
+        m0 = sp[0];
+        m1 = sp[1];
+        const uint32_t nh = wrapq(q.h + 1, S.Q);
+        const uint32_t narr = qb[nh * 8];
+        if (!have_w && n.role != RAFT_LEADER) {
+          w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+          have_w = true;
+        }
+        QueueR r = q;
+        r.h = nh;
+        r.c -= 1;
+        r.arr = r.c ? narr : INF;
+        r.tail = r.c ? r.tail : 0u;
+        if (which) n.rs = r;
+        else n.rq = r;
       }
       const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
                      mpoff = m1.w;
@@ -483,8 +518,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       if constexpr (SPEC) {
         spec_handle<N, MAJ>(S, n, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
                             emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
-                            pold_base, pold_len, preloc, pet, pev, papplied, papply_from,
-                            appended_at, elected, mchg);
+                            pold_base, preloc, papplied, elected, mchg);
       } else if (which < 0) {
         if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
           ev = 7;
@@ -554,7 +588,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               }
               ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
               pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff; ppcnt = pcnt;
-              pold_base = n.base; pold_len = n.len;
+              pold_base = n.base;
               if (pcnt) {                                    // append-entries! 61-64
                 if (n.base + n.len != n.front) {
                   preloc = 1;
@@ -562,8 +596,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                   n.front += n.len;
                 }
                 n.front += pcnt;
-                appended_at = (int)n.len;
-              }
+                        }
               const uint32_t oldc = n.commit;
               n.len += pcnt;
               n.seq = 0;
@@ -571,7 +604,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               n.commit = n.len;                              // apply-entries! 69-76
               applied = n.commit > oldc ? n.commit - oldc : 0;
               papplied = applied;
-              papply_from = oldc;
               n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;  // candidate->follower 75-78
               n.lid = src; n.term = mterm;
             }
@@ -584,16 +616,15 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               fault = RAFT_FAULT_OVERFLOW;
               break;
             }
-            pkind = PLAN_ENTRY; pet = n.term; pev = ma;
-            pold_base = n.base; pold_len = n.len;
+            pkind = PLAN_ENTRY; ppoff = n.term; ppcnt = ma;
+            pold_base = n.base;
             if (n.base + n.len != n.front) {
               preloc = 1;
               n.base = n.front;
               n.front += n.len;
             }
             n.front += 1;
-            appended_at = (int)n.len;
-            n.len += 1;
+                  n.len += 1;
             n.seq = 0;
             appended = 1;
             break;
@@ -652,7 +683,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
         pkind = PLAN_NONE;
         papplied = 0;
-        appended_at = -1;
         elected = false;
         mchg = false;
       } else {
@@ -698,6 +728,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             part = ppm(pw.x) < S.part_ppm;
             sides = pw.y;
           }
+          *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
+              emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
           if (emit == 3) {
             uint32_t* cl =
                 mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
@@ -768,17 +800,18 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       uint32_t copy = 0;
       while (inmask) {
         const int s = __builtin_ctz(inmask);
-        const uint4* cl =
-            reinterpret_cast<const uint4*>(mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
-        const uint4 a = cl[0], b = cl[1];
-        const uint32_t d = copy == 0 ? (b.w & 0xFF) : ((b.w >> 8) & 0xFF);
-        const int which = (a.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
+        const uint2* cl =
+            reinterpret_cast<const uint2*>(mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
+        const uint2 c0 = cl[0], c1 = cl[1], c2 = cl[2];
+        const uint2 sr = *reinterpret_cast<const uint2*>(mysrec + s * SRECW);
+        const uint32_t d = copy == 0 ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
+        const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
-        qinsert(S, sgi, n.fault, which, q, make_uint4(t + d, a.x, a.y, a.z),
-                make_uint4(a.w, b.x, b.y, b.z), lctr);
+        qinsert(S, sgi, n.fault, which, q, make_uint4(t + d, c0.x, sr.x, sr.y),
+                make_uint4(c0.y, c1.x, c1.y, c2.x), lctr);
         if (which) n.rs = q;
         else n.rq = q;
-        if (++copy >= (b.w >> 16)) {
+        if (++copy >= (c2.y >> 16)) {
           copy = 0;
           inmask &= inmask - 1;
         }
@@ -786,15 +819,18 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
 
     // ---------------------------------------------------------------- P3 log writes
-    if (__ballot(pkind != PLAN_NONE || papplied || (TRACE && tr_cnt))) {
+    // m entries were added at position n.len - m (appended_at, -1 when none)
+    const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
+    const int appended_at = m ? (int)(n.len - m) : -1;
+    if (__ballot(m || papplied || (TRACE && tr_cnt))) {
       const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
-      const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : 1;
-      if (pkind != PLAN_NONE && m) {
+      if (m) {
+        const uint32_t pold_len = n.len - m;
         // physical slots advance with a wrap instead of a per-entry modulo
         if (preloc) arena_copy(sar, n.base % A, sar, pold_base % A, pold_len, A);
         uint32_t di = (n.base + pold_len) % A;
         if (pkind == PLAN_ENTRY) {
-          sar[di] = make_uint2(pet, pev);
+          sar[di] = make_uint2(ppoff, ppcnt);
         } else {
           // entries i with sender frontier > poff + i + A were overwritten (SIM_SPEC P3)
           const int64_t ev = (int64_t)sfront - (int64_t)A - (int64_t)ppoff;
@@ -811,7 +847,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
       if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
         uint32_t cc = S.ccount[sgi];
-        uint32_t si = (n.base + papply_from) % A;
+        uint32_t si = (n.base + n.commit - papplied) % A;
         for (uint32_t i = 0; i < papplied; ++i, ++cc) {
           if (S.SC) S.stream[(size_t)sgi * S.SC + cc % S.SC] = sar[si].y;
           si = si + 1 == A ? 0 : si + 1;
@@ -926,7 +962,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
     S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
     S.trace_lo[gi] = (uint32_t)n.trace; S.trace_hi[gi] = (uint32_t)(n.trace >> 32);
-    if (k == 0) {
+    if (k0 == 0) {
       S.cl[c * 8] = hidx; S.cl[c * 8 + 1] = hterm; S.cl[c * 8 + 2] = hval;
       S.cl[c * 8 + 3] = cnext; S.cl[c * 8 + 4] = ccount;
     }
@@ -939,6 +975,32 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     const uint32_t v = lctr[lane];
     if (v != INF) atomicMin(&S.ctr[RAFT_CTR_COUNT], (unsigned long long)v);
   }
+}
+
+// RAFT_SCHED_ALIGNED: sort key of cluster c before a launch starting at t0 -- its next event
+// tick (min over running nodes of deadline and queue heads, and the next client-set), relative
+// to t0 and clamped to 16 bits. Clusters with the same next event then share waves, and a
+// steady-state cluster's later events (heartbeat every hb ticks) stay aligned with its wave
+// mates', so a wave's active ticks are nearly those of one cluster instead of the union of 12.
+__global__ void sched_key_kernel(DevSim S, uint32_t t0, uint32_t* keys, uint32_t* ids) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= S.C) return;
+  uint32_t m = S.cl[c * 8 + 3];
+  for (uint32_t k = 0; k < S.N; ++k) {
+    const uint32_t gi = c * S.N + k;
+    if ((S.flags[gi] >> 10) & 7) continue;
+    m = min(m, min(S.deadline[gi], min(S.req_arr[gi], S.res_arr[gi])));
+  }
+  const uint32_t d = m > t0 ? m - t0 : 0u;
+  keys[c] = d < 0xFFFFu ? d : 0xFFFFu;
+  ids[c] = c;
+}
+
+hipError_t launch_sched_key(const DevSim& S, uint32_t t0, uint32_t* keys, uint32_t* ids,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(sched_key_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, t0, keys,
+                     ids);
+  return hipGetLastError();
 }
 
 // Initial state: init-node (core.clj:31-38) and an empty log (log.clj:33-34) for every node.

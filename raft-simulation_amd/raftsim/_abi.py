@@ -27,7 +27,7 @@ class Config(C.Structure):
                 ("client_ppm", C.c_uint32), ("variant_flags", C.c_uint32),
                 ("device", C.c_int32), ("ticks_per_launch", C.c_uint32),
                 ("commit_stream_cap", C.c_uint32), ("trace_cap", C.c_uint32),
-                ("trace_entry_cap", C.c_uint32), ("reserved", C.c_uint32 * 1)]
+                ("trace_entry_cap", C.c_uint32), ("schedule", C.c_uint32)]
 
 
 class Node(C.Structure):
