@@ -4,7 +4,8 @@
 //   hot node words   flags, masks, term, commit, len, deadline, qmeta, req/res head+tail arrival,
 //                    arena base/frontier, last_led, trace lo/hi           [NN] u32 each
 //   cold node words  next_index / match_index                              [N][NN] i32
-//   queues           qbuf[gi][which][Q] of 8-word messages (ring, sorted by arrival)
+//   queues           qbuf[which][slot][gi] of 8-word messages (ring per node, sorted by arrival);
+//                    slot-major so the same ring slot of a cluster's nodes is contiguous
 //   log arenas       arena[gi][A] of (term, val)
 //   cluster words    cl[c] = raft_cluster_t (hwm index, term, val, client_next, client_count, 0,0,0)
 // A wave owns floor(64 / N) whole clusters, one lane per node; a cluster never spans waves, so all
@@ -21,7 +22,11 @@ constexpr uint32_t INF = 0xFFFFFFFFu;
 enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;  // per-wave LDS counter slot holding min tick
+#ifdef RS_WAVESTATS
+constexpr int LCTR_WORDS = 64;   // diagnostic build: + the wave's phase clock
+#else
 constexpr int LCTR_WORDS = 32;
+#endif
 constexpr int PW_WORDS = 64;   // 32 x u64 client-gap powers at the start of the block's LDS
 
 struct DevSim {
@@ -31,7 +36,7 @@ struct DevSim {
   uint32_t *flags, *masks, *term, *commit, *len, *deadline, *qmeta, *req_arr, *res_arr,
       *req_tail, *res_tail, *abase, *afront, *led, *trace_lo, *trace_hi;
   int32_t *next, *match;  // [N][NN], row p-1 for peer id p
-  uint32_t* qbuf;         // [NN][2][Q][8]
+  uint32_t* qbuf;         // [2][Q][NN][8]
   uint32_t* arena;        // [NN][A][2]
   uint32_t* cl;           // [C][8] raft_cluster_t
   uint32_t* ccount;       // [NN] commit_count (F2)
@@ -135,16 +140,20 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 
 __device__ __forceinline__ uint32_t wrapq(uint32_t x, uint32_t Q) { return x >= Q ? x - Q : x; }
 
+// Slot 0 of node gi's queue `which`; slot i is qslots(...) + i * qstride(S).
 __device__ __forceinline__ uint32_t* qslots(const DevSim& S, uint32_t gi, int which) {
-  return S.qbuf + ((size_t)gi * 2 + which) * S.Q * 8;
+  return S.qbuf + ((size_t)which * S.Q * S.NN + gi) * 8;
 }
+__device__ __forceinline__ size_t qstride(const DevSim& S) { return (size_t)S.NN * 8; }
 
 __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
   return reinterpret_cast<uint2*>(S.arena) + (size_t)gi * S.A;
 }
 
 __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
+#ifndef RS_DIAG_NOCTR
   if (v) atomicAdd(&lctr[i], v);
+#endif
 }
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own
@@ -161,15 +170,16 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
     return;
   }
   uint32_t* qb = qslots(S, gi, which);
+  const size_t qs = qstride(S);
   const uint32_t arr = m0.x, head = q.h;
   uint32_t pos = q.c;
   if (pos > 0 && arr < q.tail) {
     while (pos > 0) {
       const uint32_t prev = wrapq(head + pos - 1, Q);
-      if (qb[prev * 8] <= arr) break;
+      if (qb[prev * qs] <= arr) break;
       const uint32_t dst = wrapq(head + pos, Q);
-      uint4* sp = reinterpret_cast<uint4*>(qb + prev * 8);
-      uint4* dp = reinterpret_cast<uint4*>(qb + dst * 8);
+      uint4* sp = reinterpret_cast<uint4*>(qb + prev * qs);
+      uint4* dp = reinterpret_cast<uint4*>(qb + dst * qs);
       dp[0] = sp[0];
       dp[1] = sp[1];
       --pos;
@@ -177,7 +187,7 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
   } else {
     q.tail = arr;
   }
-  uint4* dp = reinterpret_cast<uint4*>(qb + wrapq(head + pos, Q) * 8);
+  uint4* dp = reinterpret_cast<uint4*>(qb + wrapq(head + pos, Q) * qs);
   dp[0] = m0;
   dp[1] = m1;
   q.c += 1;

@@ -255,6 +255,11 @@ static int check_range(raft_sim* s, uint32_t c0, uint32_t nc) {
   return 0;
 }
 
+// Slot 0 of node gi's queue `which` in the slot-major queue buffer [2][Q][NN] (slot stride NN).
+static uint32_t* qring(raft_sim* s, uint32_t gi, uint32_t which) {
+  return s->d.qbuf + ((size_t)which * s->Q * s->NN + gi) * 8;
+}
+
 static int check_node(raft_sim* s, uint32_t cluster, uint32_t id) {
   if (!s) return fail(-EINVAL, "null sim");
   if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
@@ -371,8 +376,9 @@ int raft_sim_read_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t w
   uint32_t qm = 0;
   std::vector<raft_msg_t> slots(s->Q);
   HIP_OK(d2h(s, &qm, s->d.qmeta + gi, 1));
-  HIP_OK(hipMemcpyAsync(slots.data(), s->d.qbuf + ((size_t)gi * 2 + which) * s->Q * 8,
-                        s->Q * sizeof(raft_msg_t), hipMemcpyDeviceToHost, s->stream));
+  HIP_OK(hipMemcpy2DAsync(slots.data(), sizeof(raft_msg_t), qring(s, gi, which),
+                          (size_t)s->NN * sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q,
+                          hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   const uint32_t head = which ? (qm >> 9) & 15 : qm & 15;
   const uint32_t cnt = which ? (qm >> 13) & 31 : (qm >> 4) & 31;
@@ -404,8 +410,9 @@ int raft_sim_write_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t 
   if (which) qm = (qm & ~(0xFu << 9 | 0x1Fu << 13)) | count << 13;
   else qm = (qm & ~0x1FFu) | count << 4;
   const uint32_t harr = count ? in[0].arrival : rs::INF, tail = count ? in[count - 1].arrival : 0;
-  HIP_OK(hipMemcpyAsync(s->d.qbuf + ((size_t)gi * 2 + which) * s->Q * 8, slots.data(),
-                        s->Q * sizeof(raft_msg_t), hipMemcpyHostToDevice, s->stream));
+  HIP_OK(hipMemcpy2DAsync(qring(s, gi, which), (size_t)s->NN * sizeof(raft_msg_t), slots.data(),
+                          sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q, hipMemcpyHostToDevice,
+                          s->stream));
   HIP_OK(h2d(s, s->d.qmeta + gi, &qm, 1));
   HIP_OK(h2d(s, (which ? s->d.res_arr : s->d.req_arr) + gi, &harr, 1));
   HIP_OK(h2d(s, (which ? s->d.res_tail : s->d.req_tail) + gi, &tail, 1));

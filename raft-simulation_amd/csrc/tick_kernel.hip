@@ -326,6 +326,22 @@ constexpr size_t block_lds_bytes() {
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
 #endif
+#ifdef RS_WAVESTATS
+// Wave-level phase clock in LDS (wst: 11 accumulators + the last stamp): every active lane
+// writes the same values, so a stamp inside a divergent region still charges the wave.
+#define RS_STAMP(i)                                        \
+  do {                                                     \
+    __builtin_amdgcn_s_waitcnt(0);                         \
+    const uint64_t now_ = clock64();                       \
+    const uint64_t last_ = wst[11];                        \
+    wst[i] += now_ - last_;                                \
+    wst[11] = now_;                                        \
+    __builtin_amdgcn_s_waitcnt(0);                         \
+  } while (0)
+#else
+#define RS_STAMP(i) do { } while (0)
+#endif
+
 template <int N, bool TRACE, bool SPEC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
@@ -344,7 +360,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
-  const uint32_t wave = blockIdx.x * 4 + wv;
+#ifndef RS_SPREAD
+#define RS_SPREAD 1
+#endif
+  // With RAFT_SCHED_ALIGNED, neighbouring wave slots hold clusters with the same next event, so
+  // they are active on the same ticks. A block's four waves therefore take slots a quarter of the
+  // grid apart: the waves sharing a CU's memory pipeline are active on different ticks.
+  const uint32_t wave = (RS_SPREAD && S.perm) ? wv * gridDim.x + blockIdx.x : blockIdx.x * 4 + wv;
   const int cs = lane / N, k0 = lane - cs * N;
   const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
   const bool active = lane < CPW * N && slot < S.C;
@@ -379,6 +401,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
+#ifdef RS_WAVESTATS
+  uint32_t wstat_active = 0;
+  uint64_t* wst = reinterpret_cast<uint64_t*>(lctr + 32);
+  if (lane < 12) wst[lane] = lane == 11 ? clock64() : 0ull;
+  __builtin_amdgcn_wave_barrier();
+#endif
 
   const uint32_t tend = t0 + nt;
   for (uint32_t t = t0;; ++t) {
@@ -387,6 +415,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // the wave jumps over them: discrete-event skipping with tick-exact results.
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
+    RS_STAMP(0);
     const bool live = active && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
     // address and shuffle index the active-tick phases use out of the tick loop, where each would
@@ -433,6 +462,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_STAMP(1);
     // ---------------------------------------------------------------- P1 one event per node
     const bool req_ok = live && (dcs || n.rq.arr <= t);
     const bool res_ok = live && n.rs.arr <= t;
@@ -477,11 +507,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // the ring is always in bounds) and used only when the queue stays non-empty.
         const QueueR q = which ? n.rs : n.rq;
         const uint32_t* qb = qslots(S, sgi, which);
-        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * 8);
+        const size_t qs = qstride(S);
+        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
         m0 = sp[0];
         m1 = sp[1];
         const uint32_t nh = wrapq(q.h + 1, S.Q);
-        const uint32_t narr = qb[nh * 8];
+        const uint32_t narr = qb[nh * qs];
         if (!have_w && n.role != RAFT_LEADER) {
           w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
           have_w = true;
@@ -494,6 +525,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (which) n.rs = r;
         else n.rq = r;
       }
+      RS_STAMP(2);
       const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
                      mpoff = m1.w;
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
@@ -694,6 +726,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
         // leader-state words (cold, in HBM)
+        RS_STAMP(3);
         if (nm == 1 || nm == 2) {
           const int32_t first_next = (int32_t)((SPEC ? n.len : n.commit) + 1);
 #pragma unroll
@@ -719,6 +752,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           lctr_add(lctr, RAFT_CTR_LEADERS, 1);
           n.led = n.term;
         }
+        RS_STAMP(4);
         // ------------------------------------------------ emission (rpc / respond)
         if (emit) {
           bool part = false;
@@ -742,6 +776,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             int32_t nxs[N];
 #pragma unroll
             for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? S.next[p * NN + sgi] : 0;
+            RS_STAMP(9);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -774,6 +809,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               }
               cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
             }
+            RS_STAMP(10);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -786,6 +822,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_STAMP(5);
     // ---------------------------------------------------------------- P2 network delivery
     if (__ballot(sentmask != 0)) {
       // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
@@ -818,6 +855,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_STAMP(6);
     // ---------------------------------------------------------------- P3 log writes
     // m entries were added at position n.len - m (appended_at, -1 when none)
     const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
@@ -868,6 +906,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_STAMP(7);
     // ---------------------------------------------------------------- P4 invariant checker
     // the majority-match scan can raise hwm only when the leader's log reaches past it
     const bool mcheck = (elected || mchg) && n.len > hidx;
@@ -949,8 +988,28 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
       }
     }
+    RS_STAMP(8);
     wnext = next_event();
+#ifdef RS_WAVESTATS
+    ++wstat_active;
+    RS_STAMP(0);
+#endif
   }
+#ifdef RS_WAVESTATS   // diagnostic build only: per-wave active ticks into two counters unused by C2
+  if (lane == 0) {
+    atomicAdd(&S.ctr[RAFT_CTR_PAYLOAD_EVICTED], (unsigned long long)wstat_active);
+    atomicMax(&S.ctr[RAFT_CTR_HALT_OVERFLOW], (unsigned long long)wstat_active);
+    const int wslot[11] = {RAFT_CTR_DROPPED, RAFT_CTR_PARTITIONED, RAFT_CTR_DUPLICATED,
+                          RAFT_CTR_OVERFLOW, RAFT_CTR_TO_HALTED, RAFT_CTR_CLIENT_INJECTED,
+                          RAFT_CTR_ENTRIES_APPLIED, RAFT_CTR_VIOL_ELECTION, RAFT_CTR_VIOL_LOG,
+                          RAFT_CTR_EV_CS, RAFT_CTR_ENTRIES_APPENDED};
+    for (int i = 0; i < 11; ++i) atomicAdd(&S.ctr[wslot[i]], (unsigned long long)wst[i]);
+    if (wstat_active > 40) atomicAdd(&S.ctr[RAFT_CTR_HALT_NPE], 1ull);
+    if (wstat_active > 60) atomicAdd(&S.ctr[RAFT_CTR_HALT_CCE], 1ull);
+    if (wstat_active > 80) atomicAdd(&S.ctr[RAFT_CTR_HALT_IOOBE], 1ull);
+    if (wstat_active > 100) atomicAdd(&S.ctr[RAFT_CTR_VIOL_COMPLETE], 1ull);
+  }
+#endif
 
   // ---------------------------------------------------------------- write back
   if (active) {
@@ -1073,7 +1132,7 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       h = fnv(h, qc[which]);
       const uint32_t* qb = qslots(S, gi, which);
       for (uint32_t i = 0; i < qc[which]; ++i) {
-        const uint32_t* m = qb + ((qh[which] + i) % S.Q) * 8;
+        const uint32_t* m = qb + ((qh[which] + i) % S.Q) * qstride(S);
         for (int j = 0; j < 8; ++j) h = fnv(h, m[j]);
       }
     }

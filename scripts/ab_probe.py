@@ -1,5 +1,5 @@
 """A/B kernel builds in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
-Usage: python scripts/ab_probe.py LIB_A LIB_B ... ; prints the median and min kernel ms per
+Usage: python scripts/ab_probe.py LIB_A LIB_B ... [--sched=0|1] [--WORKLOAD ...]; prints the median and min kernel ms per
 10k-tick launch for each build on each workload, and whether the builds agree on the state."""
 import statistics
 import sys
@@ -19,12 +19,14 @@ WORK = {
 
 def main():
     libs = [a for a in sys.argv[1:] if not a.startswith("--")]
-    only = [a[2:] for a in sys.argv[1:] if a.startswith("--")]
+    sched = [int(a[8:]) for a in sys.argv[1:] if a.startswith("--sched=")]
+    only = [a[2:] for a in sys.argv[1:] if a.startswith("--") and not a.startswith("--sched=")]
+    extra = {"schedule": sched[0]} if sched else {}
     rounds = 5
     for wname, cfg in WORK.items():
         if only and wname not in only:
             continue
-        sims = [Backend(lib, "raft_sim_", **cfg) for lib in libs]
+        sims = [Backend(lib, "raft_sim_", **cfg, **extra) for lib in libs]
         for s in sims:
             s.step(10000)                               # warm up to a steady state
         times = [[] for _ in libs]

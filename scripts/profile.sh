@@ -1,6 +1,6 @@
 # rocprofv3 passes over the bench (kernel trace, then one PMC group per pass). Usage: bash scripts/profile.sh TAG
 set -u
-TAG=${1:-r01}
+TAG=${1:-r03}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
