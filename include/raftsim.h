@@ -206,8 +206,9 @@ int raft_sim_read_counters(raft_sim_t* sim, raft_counters_t* out);
 /* Per-cluster FNV-1a-64 digest of the canonical state (SIM_SPEC §6). */
 int raft_sim_digest(raft_sim_t* sim, uint32_t c0, uint32_t nc, uint64_t* out);
 
-/* Average device time of the last raft_sim_step's tick-kernel launches (HIP events on the
- * simulator's stream) and their count; for bench.py's roofline. */
+/* Average device time of the last raft_sim_step's tick-kernel launches alone (a HIP event pair
+ * around each launch on the simulator's stream; the RAFT_SCHED_ALIGNED key and sort kernels
+ * between launches are excluded) and their count; for bench.py's roofline. */
 int raft_sim_last_step_timing(raft_sim_t* sim, double* avg_kernel_ms, uint32_t* launches);
 
 void raft_sim_destroy(raft_sim_t* sim);

@@ -51,7 +51,10 @@ struct DevSim {
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)
   const uint32_t* perm;     // [C] wave slot -> cluster (RAFT_SCHED_ALIGNED), null = identity
+  uint32_t* skey;           // [C] RAFT_SCHED_ALIGNED: cluster's next event - next launch's t0
+  uint32_t* shist;          // [SCHED_BUCKETS] histogram of skey (null: schedule fixed)
 };
+constexpr uint32_t SCHED_BUCKETS = 16384;   // keys clamp to SCHED_BUCKETS - 1
 
 // Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).
 __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,

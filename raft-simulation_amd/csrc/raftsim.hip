@@ -6,14 +6,12 @@
 #include <algorithm>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
-
 #include "device.hpp"
 
 namespace rs {
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st);
-hipError_t launch_sched_key(const DevSim& S, uint32_t t0, uint32_t* keys, uint32_t* ids,
-                            hipStream_t st);
+hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -42,15 +40,18 @@ struct raft_sim {
   uint64_t tick;
   hipStream_t stream;
   hipEvent_t ev_start, ev_stop;
+  std::vector<hipEvent_t> kev;   // per tick-kernel launch of a step: start, stop
   DevSim d;
   std::vector<void*> allocs;
-  double last_ms;
+  double last_ms, last_step_ms;
   uint32_t last_launches;
   unsigned long long* client_pw;
-  // RAFT_SCHED_ALIGNED: per-launch (next-event key, cluster) pairs, sorted into d.perm
-  uint32_t *sk_in, *sk_out, *sid_in, *sid_out;
-  void* sort_tmp;
-  size_t sort_tmp_bytes;
+  // RAFT_SCHED_ALIGNED: bucket offsets and the wave-slot -> cluster map of the next launch;
+  // keys_fresh: d.skey/d.shist hold a matching key set (from the previous tick launch). Only the
+  // first launch computes them from the state: after host writes the keys are merely stale,
+  // which changes the packing (speed), never the results.
+  uint32_t *soff, *sperm;
+  bool keys_fresh;
 };
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -105,6 +106,7 @@ void raft_sim_destroy(raft_sim_t* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   if (s->ev_start) (void)hipEventDestroy(s->ev_start);
   if (s->ev_stop) (void)hipEventDestroy(s->ev_stop);
+  for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -168,19 +170,11 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   }
   d.client_pw = s->client_pw;
   if (cfg->schedule == RAFT_SCHED_ALIGNED) {
-    if ((rc = dalloc(s, &s->sk_in, s->C)) || (rc = dalloc(s, &s->sk_out, s->C)) ||
-        (rc = dalloc(s, &s->sid_in, s->C)) || (rc = dalloc(s, &s->sid_out, s->C))) {
+    if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
+        (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) || (rc = dalloc(s, &s->sperm, s->C))) {
       raft_sim_destroy(s);
       return rc;
     }
-    size_t bytes = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->sk_in, s->sk_out, s->sid_in,
-                                           s->sid_out, (int)s->C, 0, 16) != hipSuccess ||
-        (rc = dalloc(s, reinterpret_cast<uint8_t**>(&s->sort_tmp), bytes))) {
-      raft_sim_destroy(s);
-      return rc ? rc : fail(-EIO, "hipcub radix-sort sizing failed");
-    }
-    s->sort_tmp_bytes = bytes;
   }
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -197,6 +191,7 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (e = hipMemsetAsync(d.tcount, 0, NN * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tent, 0, NN * std::max<uint32_t>(d.TE, 1) * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tecount, 0, NN * 4, s->stream)) != hipSuccess ||
+      (d.shist && (e = hipMemsetAsync(d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream)) != hipSuccess) ||
       (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
@@ -219,22 +214,35 @@ int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick + done;
     if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
-      // pack clusters with the same next event onto the same waves for this launch
-      HIP_OK(rs::launch_sched_key(s->d, t0, s->sk_in, s->sid_in, s->stream));
-      HIP_OK(hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, s->sort_tmp_bytes, s->sk_in,
-                                                s->sk_out, s->sid_in, s->sid_out, (int)s->C, 0,
-                                                16, s->stream));
-      s->d.perm = s->sid_out;
+      // pack clusters with the same next event onto the same waves for this launch: keys and
+      // histogram come from the previous tick launch, or are recomputed from the state
+      if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
+      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
+      s->d.perm = s->sperm;
+      s->keys_fresh = true;
     }
+    while (s->kev.size() < 2 * (size_t)(launches + 1)) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreate(&e));
+      s->kev.push_back(e);
+    }
+    HIP_OK(hipEventRecord(s->kev[2 * launches], s->stream));
     HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
+    HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
     done += nt;
     ++launches;
   }
   HIP_OK(hipEventRecord(s->ev_stop, s->stream));
   HIP_OK(hipEventSynchronize(s->ev_stop));
-  float ms = 0;
+  float ms = 0, kms = 0;
   HIP_OK(hipEventElapsedTime(&ms, s->ev_start, s->ev_stop));
-  s->last_ms = launches ? ms / launches : 0.0;
+  for (uint32_t i = 0; i < launches; ++i) {
+    float one = 0;
+    HIP_OK(hipEventElapsedTime(&one, s->kev[2 * i], s->kev[2 * i + 1]));
+    kms += one;
+  }
+  s->last_ms = launches ? kms / launches : 0.0;   // tick kernel alone
+  s->last_step_ms = ms;                           // + the schedule's key and sort kernels
   s->last_launches = launches;
   s->tick += n_ticks;
   return 0;

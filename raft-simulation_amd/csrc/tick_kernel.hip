@@ -1012,6 +1012,20 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #endif
 
   // ---------------------------------------------------------------- write back
+  if (S.shist) {
+    // RAFT_SCHED_ALIGNED: the cluster's next event relative to the next launch, counted into the
+    // bucket histogram the host turns into the next launch's wave packing (sched_scan/scatter)
+    const uint32_t me = active && !n.fault ? min(n.deadline, min(n.rq.arr, n.rs.arr)) : INF;
+    uint32_t cm = active ? cnext : INF;
+#pragma unroll
+    for (int s = 0; s < N; ++s) cm = min(cm, (uint32_t)__shfl(me, bl0 + s));
+    if (active && k0 == 0) {
+      const uint32_t d = cm > tend ? cm - tend : 0u;
+      const uint32_t key = d < SCHED_BUCKETS - 1 ? d : SCHED_BUCKETS - 1;
+      S.skey[c] = key;
+      atomicAdd(&S.shist[key], 1u);
+    }
+  }
   if (active) {
     S.flags[gi] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
     S.masks[gi] = n.votes | n.keys << 16;
@@ -1036,12 +1050,16 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   }
 }
 
-// RAFT_SCHED_ALIGNED: sort key of cluster c before a launch starting at t0 -- its next event
-// tick (min over running nodes of deadline and queue heads, and the next client-set), relative
-// to t0 and clamped to 16 bits. Clusters with the same next event then share waves, and a
-// steady-state cluster's later events (heartbeat every hb ticks) stay aligned with its wave
-// mates', so a wave's active ticks are nearly those of one cluster instead of the union of 12.
-__global__ void sched_key_kernel(DevSim S, uint32_t t0, uint32_t* keys, uint32_t* ids) {
+// RAFT_SCHED_ALIGNED wave packing: a counting sort of the clusters by their next event tick
+// (min over running nodes of deadline and queue heads, and the next client-set) relative to the
+// launch's first tick. Clusters with the same next event then share waves, and a steady-state
+// cluster's later events (heartbeat every hb ticks) stay aligned with its wave mates', so a
+// wave's active ticks are nearly those of one cluster instead of the union of twelve. The order
+// inside a bucket is whatever the scatter's atomics give: any packing yields identical results.
+//
+// sched_key_kernel: keys + histogram from the state (first launch, or after host writes);
+// the tick kernel writes both at its end for the next launch.
+__global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= S.C) return;
   uint32_t m = S.cl[c * 8 + 3];
@@ -1051,14 +1069,55 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0, uint32_t* keys, uint32_t
     m = min(m, min(S.deadline[gi], min(S.req_arr[gi], S.res_arr[gi])));
   }
   const uint32_t d = m > t0 ? m - t0 : 0u;
-  keys[c] = d < 0xFFFFu ? d : 0xFFFFu;
-  ids[c] = c;
+  const uint32_t key = d < SCHED_BUCKETS - 1 ? d : SCHED_BUCKETS - 1;
+  S.skey[c] = key;
+  atomicAdd(&S.shist[key], 1u);
 }
 
-hipError_t launch_sched_key(const DevSim& S, uint32_t t0, uint32_t* keys, uint32_t* ids,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(sched_key_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, t0, keys,
-                     ids);
+// One block: exclusive scan of the histogram into off[], which the scatter consumes; the
+// histogram is cleared for the tick kernel to refill.
+__global__ void __launch_bounds__(1024) sched_scan_kernel(uint32_t* hist, uint32_t* off) {
+  constexpr uint32_t PER = SCHED_BUCKETS / 1024;
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    v[i] = hist[t * PER + i];
+    hist[t * PER + i] = 0;
+    sum += v[i];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {        // Hillis-Steele inclusive scan
+    const uint32_t x = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    off[t * PER + i] = run;
+    run += v[i];
+  }
+}
+
+__global__ void sched_scatter_kernel(DevSim S, uint32_t* off, uint32_t* perm) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= S.C) return;
+  perm[atomicAdd(&off[S.skey[c]], 1u)] = c;
+}
+
+hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
+  hipLaunchKernelGGL(sched_key_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, t0);
+  return hipGetLastError();
+}
+
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st) {
+  hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(1024), 0, st, S.shist, off);
+  hipLaunchKernelGGL(sched_scatter_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, off,
+                     perm);
   return hipGetLastError();
 }
 
