@@ -74,11 +74,23 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
+// A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are
+// [N][NN] (row per peer); kernels with a small N keep the wave's rows in LDS for the whole launch
+// (NM_LDS below) so heartbeats and append-responses pay no global round trip for them.
+struct PeerW {
+  int32_t* nx;
+  int32_t* mt;
+  uint32_t stride;
+  __device__ __forceinline__ int32_t& next(uint32_t p) const { return nx[p * stride]; }
+  __device__ __forceinline__ int32_t& match(uint32_t p) const { return mt[p * stride]; }
+};
+
 // F3: record one `wait` iteration (core.clj:182-186) — the node map before the handler and the
 // message alts!! returned — as a raft_trace_event_t (32 words) in the node's ring.
 template <int N>
 __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint32_t t,
-                                             const NodeR& n, uint4 m0, uint4 m1, uint32_t tes) {
+                                             const NodeR& n, const PeerW& lsw, uint4 m0, uint4 m1,
+                                             uint32_t tes) {
   const uint32_t seq = S.tcount[gi];
   S.tcount[gi] = seq + 1;
   uint32_t w[32];
@@ -90,8 +102,8 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   w[12] = n.term;
 #pragma unroll
   for (int p = 0; p < RAFT_MAX_NODES; ++p) {
-    w[13 + p] = p < N ? (uint32_t)S.next[p * S.NN + gi] : 0u;
-    w[22 + p] = p < N ? (uint32_t)S.match[p * S.NN + gi] : 0u;
+    w[13 + p] = p < N ? (uint32_t)lsw.next(p) : 0u;
+    w[22 + p] = p < N ? (uint32_t)lsw.match(p) : 0u;
   }
   w[31] = tes;
   uint4* rec = reinterpret_cast<uint4*>(S.tr + ((size_t)gi * S.TC + seq % S.TC) * 32);
@@ -143,12 +155,13 @@ __device__ __forceinline__ void arena_copy(uint2* dst, uint32_t di, const uint2*
 // emission (emit/ra/rb), the leader-state writes (nm) and the P3 log plan.
 template <int N, uint32_t MAJ>
 __device__ __forceinline__ void spec_handle(
-    const DevSim& S, NodeR& n, const uint2* sar, const uint32_t* fr, uint32_t* lctr, int which,
+    const DevSim& S, NodeR& n, const PeerW& lsw, const uint2* sar, const uint32_t* fr,
+    uint32_t* lctr, int which,
     uint32_t id, int k, int bl, uint32_t sgi, uint32_t peers, uint4 m0, uint4 m1,
     uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
     uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
     uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg) {
-  const uint32_t A = S.A, NN = S.NN;
+  const uint32_t A = S.A;
   if (which < 0) {
     if (n.role == RAFT_LEADER) {                                  // heartbeat
       ev = 7;
@@ -284,7 +297,7 @@ __device__ __forceinline__ void spec_handle(
 #pragma unroll
       for (int p = 1; p <= N; ++p)
         vals[p - 1] = p == (int)id ? (int32_t)n.len
-                                   : (p == (int)src ? (int32_t)mb : S.match[(p - 1) * NN + sgi]);
+                                   : (p == (int)src ? (int32_t)mb : lsw.match(p - 1));
 #pragma unroll
       for (int i = 1; i < N; ++i)
 #pragma unroll
@@ -312,9 +325,13 @@ template <int N>
 constexpr int pair_words() { return (64 / N) * N * (N - 1) * CELLW; }
 template <int N>
 constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
+// NM_LDS: the wave's next_index / match_index rows live in LDS during a launch ([2][N][64]
+// words), for the N whose block then still fits four per CU.
+template <int N>
+constexpr bool nm_lds() { return N <= 5; }
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
-  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0);
+  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0);
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -358,6 +375,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   uint32_t* cells = smem + PW_WORDS + wv * WAVE_WORDS;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
+  int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
 
 #ifndef RS_SPREAD
@@ -392,6 +410,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
     hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
     cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
+    if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
+#pragma unroll
+      for (int p = 0; p < N; ++p) {
+        nmL[p * 64 + lane] = S.next[p * NN + gi];
+        nmL[(N + p) * 64 + lane] = S.match[p * NN + gi];
+      }
+    }
   }
 
   // Earliest tick at which any lane of the wave can have an event (deadline or queue head);
@@ -428,6 +453,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t* const mycells = cells + bl * (N - 1) * CELLW;
     uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
     uint2* const sar = arena_of(S, sgi);
+    const PeerW lsw = nm_lds<N>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
+                                 : PeerW{S.next + sgi, S.match + sgi, NN};
     if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
       fr[lane] = n.front;
       __builtin_amdgcn_wave_barrier();
@@ -532,7 +559,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                      mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
       if constexpr (TRACE) {
         const uint32_t tes = S.tecount[sgi];
-        trace_record<N>(S, sgi, t, n, m0, m1, tes);
+        trace_record<N>(S, sgi, t, n, lsw, m0, m1, tes);
         if (which >= 0 && type == RAFT_MSG_APPEND_ENTRIES && pcnt) {
           tr_cnt = pcnt; tr_src = src; tr_poff = mpoff; tr_at = tes;
           S.tecount[sgi] = tes + pcnt;
@@ -548,7 +575,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       uint32_t appended = 0, applied = 0;
 
       if constexpr (SPEC) {
-        spec_handle<N, MAJ>(S, n, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
+        spec_handle<N, MAJ>(S, n, lsw, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
                             emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
                             pold_base, preloc, papplied, elected, mchg);
       } else if (which < 0) {
@@ -731,19 +758,19 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           const int32_t first_next = (int32_t)((SPEC ? n.len : n.commit) + 1);
 #pragma unroll
           for (int p = 1; p <= N; ++p) {
-            S.next[(p - 1) * NN + sgi] = (nm == 1 && p != (int)id) ? first_next : 0;
-            S.match[(p - 1) * NN + sgi] = 0;
+            lsw.next(p - 1) = (nm == 1 && p != (int)id) ? first_next : 0;
+            lsw.match(p - 1) = 0;
           }
         } else if (nm == 3) {
           if constexpr (SPEC) {
-            const int32_t nx = S.next[(src - 1) * NN + sgi] - 1;
-            S.next[(src - 1) * NN + sgi] = nx > 1 ? nx : 1;
+            const int32_t nx = lsw.next(src - 1) - 1;
+            lsw.next(src - 1) = nx > 1 ? nx : 1;
           } else {
-            S.next[(src - 1) * NN + sgi] -= 1;
+            lsw.next(src - 1) -= 1;
           }
         } else if (nm == 4) {
-          S.next[(src - 1) * NN + sgi] = (int32_t)(SPEC ? mb + 1 : mb);
-          S.match[(src - 1) * NN + sgi] = (int32_t)(SPEC ? mb : ma);
+          lsw.next(src - 1) = (int32_t)(SPEC ? mb + 1 : mb);
+          lsw.match(src - 1) = (int32_t)(SPEC ? mb : ma);
         }
         lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
@@ -775,7 +802,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             // one memory round trip per peer; the fault draws follow in a compact loop.
             int32_t nxs[N];
 #pragma unroll
-            for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? S.next[p * NN + sgi] : 0;
+            for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? lsw.next(p) : 0;
             RS_STAMP(9);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
@@ -957,7 +984,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #pragma unroll
         for (int p = 1; p <= N; ++p) {
           if (p == (int)id) continue;
-          vals[j++] = ((n.keys >> p) & 1) ? S.match[(p - 1) * NN + sgi] : 0;
+          vals[j++] = ((n.keys >> p) & 1) ? lsw.match(p - 1) : 0;
         }
 #pragma unroll
         for (int i = 1; i < N; ++i)
@@ -1035,6 +1062,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
     S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
     S.trace_lo[gi] = (uint32_t)n.trace; S.trace_hi[gi] = (uint32_t)(n.trace >> 32);
+    if constexpr (nm_lds<N>()) {
+#pragma unroll
+      for (int p = 0; p < N; ++p) {
+        S.next[p * NN + gi] = nmL[p * 64 + lane];
+        S.match[p * NN + gi] = nmL[(N + p) * 64 + lane];
+      }
+    }
     if (k0 == 0) {
       S.cl[c * 8] = hidx; S.cl[c * 8 + 1] = hterm; S.cl[c * 8 + 2] = hval;
       S.cl[c * 8 + 3] = cnext; S.cl[c * 8 + 4] = ccount;
