@@ -20,9 +20,12 @@ WORK = {
 def main():
     libs = [a for a in sys.argv[1:] if not a.startswith("--")]
     sched = [int(a[8:]) for a in sys.argv[1:] if a.startswith("--sched=")]
-    only = [a[2:] for a in sys.argv[1:] if a.startswith("--") and not a.startswith("--sched=")]
+    only = [a[2:] for a in sys.argv[1:]
+            if a.startswith("--") and not a.startswith(("--sched=", "--rounds="))]
     extra = {"schedule": sched[0]} if sched else {}
     rounds = 5
+    rr = [int(a[9:]) for a in sys.argv[1:] if a.startswith("--rounds=")]
+    rounds = rr[0] if rr else rounds
     for wname, cfg in WORK.items():
         if only and wname not in only:
             continue
