@@ -108,12 +108,14 @@ def main():
     c_before = sim.counters()
     sync()
     t0 = time.perf_counter()
-    kernel_ms, launches = 0.0, 0
+    # K steps enqueued back to back on the simulator's stream (raft_sim_step_async), then one
+    # raft_sim_sync: the host does not wait between steps; per-launch HIP events still time
+    # every tick-kernel launch of the K steps
     for _ in range(args.steps):
-        sim.step(TICKS_PER_STEP)          # synchronous: returns after the stream drains
-        ms, n = sim.last_step_timing()
-        kernel_ms += ms * n
-        launches += n
+        sim.step_async(TICKS_PER_STEP)
+    sim.sync()
+    ms, launches = sim.last_step_timing()
+    kernel_ms = ms * launches
     sync()
     elapsed = time.perf_counter() - t0
     c_after = sim.counters()

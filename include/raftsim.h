@@ -160,6 +160,13 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out);
  * node of every cluster: advances all clusters by n_ticks (synchronous). */
 int raft_sim_step(raft_sim_t* sim, uint32_t n_ticks);
 
+/* raft_sim_step without the wait: enqueues the launches for n_ticks on the simulator's stream and
+ * returns. Reads, digests and the next step are stream-ordered after it; raft_sim_sync waits for
+ * everything enqueued and makes raft_sim_last_step_timing cover those launches. Many steps
+ * queued between syncs pay no host round trip per step. */
+int raft_sim_step_async(raft_sim_t* sim, uint32_t n_ticks);
+int raft_sim_sync(raft_sim_t* sim);
+
 /* Ticks simulated so far (the next tick to run). */
 uint64_t raft_sim_tick(const raft_sim_t* sim);
 
@@ -206,9 +213,10 @@ int raft_sim_read_counters(raft_sim_t* sim, raft_counters_t* out);
 /* Per-cluster FNV-1a-64 digest of the canonical state (SIM_SPEC §6). */
 int raft_sim_digest(raft_sim_t* sim, uint32_t c0, uint32_t nc, uint64_t* out);
 
-/* Average device time of the last raft_sim_step's tick-kernel launches alone (a HIP event pair
- * around each launch on the simulator's stream; the RAFT_SCHED_ALIGNED key and sort kernels
- * between launches are excluded) and their count; for bench.py's roofline. */
+/* Average device time of the tick-kernel launches of the last raft_sim_step (or of every
+ * raft_sim_step_async since the previous sync, once raft_sim_sync returned) alone -- a HIP event
+ * pair around each launch on the simulator's stream; the RAFT_SCHED_ALIGNED scan/scatter kernels
+ * between launches are excluded -- and their count; for bench.py's roofline. */
 int raft_sim_last_step_timing(raft_sim_t* sim, double* avg_kernel_ms, uint32_t* launches);
 
 void raft_sim_destroy(raft_sim_t* sim);

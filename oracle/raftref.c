@@ -181,6 +181,8 @@ void raft_ref_destroy(raft_ref_t* s) {
 }
 
 uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
+int raft_ref_step_async(raft_ref_t* s, uint32_t n_ticks) { return raft_ref_step(s, n_ticks); }
+int raft_ref_sync(raft_ref_t* s) { return s ? 0 : fail(-EINVAL, "null sim"); }
 
 /* ---------------------------------------------------------------- per-cluster tick */
 typedef struct {

@@ -29,6 +29,8 @@ void raft_ref_default_config(raft_sim_config_t* cfg);
 int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out);
 int raft_ref_set_threads(raft_ref_t* sim, int threads);
 int raft_ref_step(raft_ref_t* sim, uint32_t n_ticks);
+int raft_ref_step_async(raft_ref_t* sim, uint32_t n_ticks);   /* = raft_ref_step (CPU) */
+int raft_ref_sync(raft_ref_t* sim);                             /* no-op */
 uint64_t raft_ref_tick(const raft_ref_t* sim);
 int raft_ref_read_nodes(raft_ref_t* sim, uint32_t c0, uint32_t nc, raft_node_t* out);
 int raft_ref_write_nodes(raft_ref_t* sim, uint32_t c0, uint32_t nc, const raft_node_t* in);

@@ -44,6 +44,8 @@ struct raft_sim {
   DevSim d;
   std::vector<void*> allocs;
   double last_ms, last_step_ms;
+  bool pending;                  // launches enqueued since the last sync
+  uint32_t pending_launches;
   uint32_t last_launches;
   unsigned long long* client_pw;
   // RAFT_SCHED_ALIGNED: bucket offsets and the wave-slot -> cluster map of the next launch;
@@ -204,12 +206,16 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   return 0;
 }
 
-int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
+int raft_sim_step_async(raft_sim_t* s, uint32_t n_ticks) {
   if (!s) return fail(-EINVAL, "null sim");
   if (s->tick + n_ticks > 0xFFFFFFFFull) return fail(-EINVAL, "tick counter would exceed 2^32");
   HIP_OK(hipSetDevice(s->cfg.device));
-  uint32_t launches = 0;
-  HIP_OK(hipEventRecord(s->ev_start, s->stream));
+  uint32_t launches = s->pending_launches;
+  if (!s->pending) {
+    HIP_OK(hipEventRecord(s->ev_start, s->stream));
+    launches = 0;
+    s->pending = true;
+  }
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick + done;
@@ -231,7 +237,22 @@ int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
     HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
     done += nt;
     ++launches;
+    s->pending_launches = launches;
   }
+  s->tick += n_ticks;
+  return 0;
+}
+
+int raft_sim_sync(raft_sim_t* s) {
+  if (!s) return fail(-EINVAL, "null sim");
+  HIP_OK(hipSetDevice(s->cfg.device));
+  if (!s->pending) {
+    HIP_OK(hipStreamSynchronize(s->stream));
+    return 0;
+  }
+  const uint32_t launches = s->pending_launches;
+  s->pending = false;
+  s->pending_launches = 0;
   HIP_OK(hipEventRecord(s->ev_stop, s->stream));
   HIP_OK(hipEventSynchronize(s->ev_stop));
   float ms = 0, kms = 0;
@@ -244,8 +265,12 @@ int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
   s->last_ms = launches ? kms / launches : 0.0;   // tick kernel alone
   s->last_step_ms = ms;                           // + the schedule's key and sort kernels
   s->last_launches = launches;
-  s->tick += n_ticks;
   return 0;
+}
+
+int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
+  const int rc = raft_sim_step_async(s, n_ticks);
+  return rc ? rc : raft_sim_sync(s);
 }
 
 int raft_sim_last_step_timing(raft_sim_t* s, double* avg_kernel_ms, uint32_t* launches) {

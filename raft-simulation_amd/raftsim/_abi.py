@@ -105,6 +105,8 @@ _SIGS = {
     "default_config": (None, [P(Config)]),
     "create": (C.c_int, [P(Config), P(C.c_void_p)]),
     "step": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "step_async": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sync": (C.c_int, [C.c_void_p]),
     "tick": (C.c_uint64, [C.c_void_p]),
     "read_nodes": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Node)]),
     "write_nodes": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Node)]),

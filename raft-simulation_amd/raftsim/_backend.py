@@ -68,6 +68,13 @@ class Backend:
     def step(self, n_ticks):
         self._check(self._fns["step"](self._h, int(n_ticks)))
 
+    def step_async(self, n_ticks):
+        """Enqueue n_ticks without waiting (the oracle runs them at once); see sync()."""
+        self._check(self._fns["step_async"](self._h, int(n_ticks)))
+
+    def sync(self):
+        self._check(self._fns["sync"](self._h))
+
     @property
     def tick(self):
         return int(self._fns["tick"](self._h))

@@ -193,3 +193,21 @@ def test_gpu_schedule_invariance(cfg):
         b.step(5000)
         assert np.array_equal(a.digest(), b.digest())
         assert a.counters() == b.counters()
+
+
+@pytest.mark.gpu
+def test_gpu_step_async_matches_step():
+    """K raft_sim_step_async calls + one raft_sim_sync leave the same state, counters and tick as
+    K synchronous raft_sim_step calls, and the timing covers every launch of the K steps."""
+    cfg = dict(n_clusters=2048, nodes=5, seed=9, client_ppm=5000, log_cap=128,
+               ticks_per_launch=3000, **FAULTS)
+    a, b = helpers.gpu(**cfg), helpers.gpu(**cfg)
+    for _ in range(4):
+        a.step(5000)
+        b.step_async(5000)
+    b.sync()
+    assert a.tick == b.tick == 20000
+    assert np.array_equal(a.digest(), b.digest())
+    assert a.counters() == b.counters()
+    ms, launches = b.last_step_timing()
+    assert launches == 8 and ms > 0
