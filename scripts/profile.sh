@@ -1,11 +1,11 @@
 # rocprofv3 passes over the bench (kernel trace, then one PMC group per pass). Usage: bash scripts/profile.sh TAG
 set -u
-TAG=${1:-r03}
+TAG=${1:-r04}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+B="python3 $R/bench.py --steps 12 --warmup 2 --no-cpu-baseline"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- $B > $OUT/kt.log 2>&1 || { echo "kt failed $?"; exit 1; }
 echo "kt ok"
 i=0
