@@ -161,16 +161,17 @@ __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own
 // queue `which` (SIM_SPEC §4 P2: after every queued message whose arrival <= the new one).
-__device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
+// Returns true when the message became the queue's head (the caller's head-register copy).
+__device__ __forceinline__ bool qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
                                         QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr) {
   if (fault) {
     lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
-    return;
+    return false;
   }
   const uint32_t Q = S.Q;
   if (q.c >= Q) {
     lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
-    return;
+    return false;
   }
   uint32_t* qb = qslots(S, gi, which);
   const size_t qs = qstride(S);
@@ -196,6 +197,7 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
   q.c += 1;
   if (pos == 0) q.arr = arr;
   lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+  return pos == 0;
 }
 
 }  // namespace rs

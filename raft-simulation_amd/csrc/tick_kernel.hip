@@ -340,6 +340,12 @@ constexpr size_t block_lds_bytes() {
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
 // faithful kernel carries none of its code.
+#ifndef RS_QRESET
+#define RS_QRESET 1
+#endif
+#ifndef RS_HEADREG
+#define RS_HEADREG 0
+#endif
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
 #endif
@@ -395,6 +401,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   const uint32_t NN = S.NN, A = S.A;
 
   NodeR n = {};
+  // Head registers (RS_HEADREG bit 0 REQ, bit 1 RES): while a queue is non-empty, its head
+  // message is also held here (words y..w of m0, all of m1; m0.x is the queue's `arr`). The queue
+  // in HBM stays complete (write-through), so a pop needs no load on its critical path; the new
+  // head is loaded at the pop and is not waited on until the next pop.
+  constexpr bool HRQ = (RS_HEADREG & 1) != 0, HRS = (RS_HEADREG & 2) != 0;
+  uint4 rqh0 = make_uint4(0, 0, 0, 0), rqh1 = rqh0, rsh0 = rqh0, rsh1 = rqh0;
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
   uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
   if (active) {
@@ -408,6 +420,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     n.rq.tail = S.req_tail[gi]; n.rs.tail = S.res_tail[gi];
     n.base = S.abase[gi]; n.front = S.afront[gi]; n.led = S.led[gi];
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
+    if (HRQ && n.rq.c) {
+      const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 0) + n.rq.h * qstride(S));
+      rqh0 = hp[0]; rqh1 = hp[1];
+    }
+    if (HRS && n.rs.c) {
+      const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 1) + n.rs.h * qstride(S));
+      rsh0 = hp[0]; rsh1 = hp[1];
+    }
     hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
     cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
     if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
@@ -426,6 +446,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
+#ifdef RS_WAVETIME
+  const uint64_t wt0 = wall_clock64();
+  uint32_t wt_active = 0;
+#endif
 #ifdef RS_WAVESTATS
   uint32_t wstat_active = 0;
   uint64_t* wst = reinterpret_cast<uint64_t*>(lctr + 32);
@@ -441,6 +465,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
     RS_STAMP(0);
+#ifdef RS_WAVETIME
+    ++wt_active;
+#endif
     const bool live = active && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
     // address and shuffle index the active-tick phases use out of the tick loop, where each would
@@ -484,8 +511,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (__ballot(inj)) {
       if (inj) {
         if (live && n.rq.c == 0) dcs = true;
-        else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                     make_uint4(0, 0, 0, 0), lctr);
+        else if (qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                         make_uint4(0, 0, 0, 0), lctr) && HRQ) {
+          rqh0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
+          rqh1 = make_uint4(0, 0, 0, 0);
+        }
       }
     }
 
@@ -523,8 +553,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
           lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
         } else {
-          qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                  make_uint4(0, 0, 0, 0), lctr);
+          if (qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                      make_uint4(0, 0, 0, 0), lctr) && HRQ) {
+            rqh0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
+            rqh1 = make_uint4(0, 0, 0, 0);
+          }
         }
       }
       if (which >= 0 && !(dcs && which == 0)) {
@@ -535,11 +568,41 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const QueueR q = which ? n.rs : n.rq;
         const uint32_t* qb = qslots(S, sgi, which);
         const size_t qs = qstride(S);
-        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
-        m0 = sp[0];
-        m1 = sp[1];
+        const bool hreg = which ? HRS : HRQ;
+        if (hreg) {
+          const uint4 h0 = which ? rsh0 : rqh0;
+          m0 = make_uint4(q.arr, h0.y, h0.z, h0.w);
+          m1 = which ? rsh1 : rqh1;
+        } else {
+          const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
+          m0 = sp[0];
+          m1 = sp[1];
+        }
         const uint32_t nh = wrapq(q.h + 1, S.Q);
+#if RS_QRESET
+        // Only a queue that stays non-empty has a next head. Its arrival is known without a load
+        // when one message remains or all queued ones share the head's arrival (the queue is
+        // sorted, so head == tail means all equal): then nothing this tick waits on memory.
+        uint32_t narr = INF;
+        if (q.c > 1) {
+          if (q.c == 2 || q.arr == q.tail) narr = q.tail;
+          else narr = qb[nh * qs];
+          if (hreg) {
+            const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
+            const uint4 n0 = np[0], n1 = np[1];
+            if (which) { rsh0 = n0; rsh1 = n1; }
+            else { rqh0 = n0; rqh1 = n1; }
+          }
+        }
+#else
         const uint32_t narr = qb[nh * qs];
+        if (hreg) {
+          const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
+          const uint4 n0 = np[0], n1 = np[1];
+          if (which) { rsh0 = n0; rsh1 = n1; }
+          else { rqh0 = n0; rqh1 = n1; }
+        }
+#endif
         if (!have_w && n.role != RAFT_LEADER) {
           w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
           have_w = true;
@@ -549,6 +612,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         r.c -= 1;
         r.arr = r.c ? narr : INF;
         r.tail = r.c ? r.tail : 0u;
+#if RS_QRESET
+        // A queue that drains restarts its ring at slot 0 (the ring position is not state: reads
+        // linearise from the head). Steady-state traffic then lands in slots 0..P-1, where a
+        // cluster's nodes are adjacent, instead of walking all Q slots of the [slot][node] layout.
+        if (!r.c) r.h = 0;
+#endif
         if (which) n.rs = r;
         else n.rq = r;
       }
@@ -871,10 +940,15 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const uint32_t d = copy == 0 ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
         const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
-        qinsert(S, sgi, n.fault, which, q, make_uint4(t + d, c0.x, sr.x, sr.y),
-                make_uint4(c0.y, c1.x, c1.y, c2.x), lctr);
-        if (which) n.rs = q;
-        else n.rq = q;
+        const uint4 q0 = make_uint4(t + d, c0.x, sr.x, sr.y), q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
+        const bool nhd = qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
+        if (which) {
+          n.rs = q;
+          if (HRS && nhd) { rsh0 = q0; rsh1 = q1; }
+        } else {
+          n.rq = q;
+          if (HRQ && nhd) { rqh0 = q0; rqh1 = q1; }
+        }
         if (++copy >= (c2.y >> 16)) {
           copy = 0;
           inmask &= inmask - 1;
@@ -1075,13 +1149,34 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#ifdef RS_DIAG_NOFLUSH
+  if (false) {
+#else
   if (lane < RAFT_CTR_COUNT) {
+#endif
     const uint32_t v = lctr[lane];
     if (v) atomicAdd(&S.ctr[lane], (unsigned long long)v);
   } else if (lane == LCTR_FIRSTVIOL) {
     const uint32_t v = lctr[lane];
     if (v != INF) atomicMin(&S.ctr[RAFT_CTR_COUNT], (unsigned long long)v);
   }
+#ifdef RS_WAVETIME   // diagnostic build: wave lifetime (100 MHz ticks) into counters C2 never uses
+  if (lane == 0 && t0 > 0) {
+    const unsigned long long dur = wall_clock64() - wt0;
+    const bool slow = dur >= 15000;
+    atomicAdd(&S.ctr[RAFT_CTR_DROPPED], dur);
+    atomicAdd(&S.ctr[RAFT_CTR_PARTITIONED], (unsigned long long)wt_active);
+    if (slow) {
+      atomicAdd(&S.ctr[RAFT_CTR_DUPLICATED], 1ull);
+      atomicAdd(&S.ctr[RAFT_CTR_OVERFLOW], (unsigned long long)wt_active);
+      atomicAdd(&S.ctr[RAFT_CTR_CLIENT_INJECTED], dur);
+      if (wave >= 4096) atomicAdd(&S.ctr[RAFT_CTR_ENTRIES_APPLIED], 1ull);
+    }
+    atomicMax(&S.ctr[RAFT_CTR_TO_HALTED],
+              (unsigned long long)dur << 40 | (unsigned long long)(wt_active & 0xFFFF) << 24 | wave);
+    if (wt_active > 40) atomicAdd(&S.ctr[RAFT_CTR_VIOL_ELECTION], 1ull);
+  }
+#endif
 }
 
 // RAFT_SCHED_ALIGNED wave packing: a counting sort of the clusters by their next event tick
