@@ -34,6 +34,10 @@ static int fail(int code, const char* fmt, const char* detail = "") {
                                       hipGetErrorString(e_));                      \
   } while (0)
 
+#ifndef RS_RESORT_EVERY
+#define RS_RESORT_EVERY 1
+#endif
+
 struct raft_sim {
   raft_sim_config_t cfg;
   uint32_t N, Q, L, A, C, NN, tpl;
@@ -54,6 +58,10 @@ struct raft_sim {
   // which changes the packing (speed), never the results.
   uint32_t *soff, *sperm;
   bool keys_fresh;
+  // the packing is rebuilt before every RS_RESORT_EVERY-th launch (and the first): steady-state
+  // clusters keep their phase relationship (equal heartbeat periods), so a packing stays aligned
+  // over several launches and the key/histogram/scan/scatter work is paid once per K launches
+  uint32_t nlaunch;
 };
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -219,21 +227,33 @@ int raft_sim_step_async(raft_sim_t* s, uint32_t n_ticks) {
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick + done;
+    rs::DevSim dl = s->d;
     if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
       // pack clusters with the same next event onto the same waves for this launch: keys and
       // histogram come from the previous tick launch, or are recomputed from the state
-      if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
-      s->d.perm = s->sperm;
-      s->keys_fresh = true;
+      if (!s->d.perm || s->nlaunch % RS_RESORT_EVERY == 0) {
+        if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
+        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
+        s->d.perm = s->sperm;
+        dl.perm = s->sperm;
+        s->keys_fresh = true;
+      }
+      // only the launch before a rebuild writes keys and histogram for it
+      if ((s->nlaunch + 1) % RS_RESORT_EVERY != 0) {
+        dl.shist = nullptr;
+        s->keys_fresh = false;
+      } else {
+        s->keys_fresh = true;
+      }
     }
+    ++s->nlaunch;
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;
       HIP_OK(hipEventCreate(&e));
       s->kev.push_back(e);
     }
     HIP_OK(hipEventRecord(s->kev[2 * launches], s->stream));
-    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
+    HIP_OK(rs::launch_tick(dl, t0, nt, s->stream));
     HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
     done += nt;
     ++launches;

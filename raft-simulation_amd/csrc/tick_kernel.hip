@@ -74,6 +74,40 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
+// Head-register cache of one queue (RS_HEADREG): while the queue is non-empty, m0.y..w and m1
+// of its head message. `dirty`: the head exists only here (it landed in an empty queue and
+// nothing has been queued behind it yet) and is written to its ring slot only when a second
+// message arrives or the launch ends; a steady-state message that is popped on the next tick
+// never reaches memory.
+struct HeadR {
+  uint4 m0, m1;
+  bool dirty;
+};
+
+template <bool HR>
+__device__ __forceinline__ bool qpush(const DevSim& S, uint32_t gi, uint32_t fault, int which,
+                                      QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr, HeadR& h) {
+  if constexpr (!HR) {
+    return qinsert(S, gi, fault, which, q, m0, m1, lctr);
+  } else {
+    if (!fault && q.c == 0) {       // as qinsert into an empty queue, without the store
+      h.m0 = m0; h.m1 = m1; h.dirty = true;
+      q.c = 1; q.arr = m0.x; q.tail = m0.x;
+      lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+      return true;
+    }
+    if (h.dirty && !fault) {
+      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, which) + q.h * qstride(S));
+      hp[0] = make_uint4(q.arr, h.m0.y, h.m0.z, h.m0.w);
+      hp[1] = h.m1;
+      h.dirty = false;
+    }
+    const bool nh = qinsert(S, gi, fault, which, q, m0, m1, lctr);
+    if (nh) { h.m0 = m0; h.m1 = m1; }
+    return nh;
+  }
+}
+
 // A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are
 // [N][NN] (row per peer); kernels with a small N keep the wave's rows in LDS for the whole launch
 // (NM_LDS below) so heartbeats and append-responses pay no global round trip for them.
@@ -343,6 +377,9 @@ constexpr size_t block_lds_bytes() {
 #ifndef RS_QRESET
 #define RS_QRESET 1
 #endif
+#ifndef RS_SCHED_FUSED
+#define RS_SCHED_FUSED 0
+#endif
 #ifndef RS_HEADREG
 #define RS_HEADREG 0
 #endif
@@ -406,7 +443,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   // in HBM stays complete (write-through), so a pop needs no load on its critical path; the new
   // head is loaded at the pop and is not waited on until the next pop.
   constexpr bool HRQ = (RS_HEADREG & 1) != 0, HRS = (RS_HEADREG & 2) != 0;
-  uint4 rqh0 = make_uint4(0, 0, 0, 0), rqh1 = rqh0, rsh0 = rqh0, rsh1 = rqh0;
+  HeadR hq = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), false}, hs = hq;
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
   uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
   if (active) {
@@ -422,11 +459,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
     if (HRQ && n.rq.c) {
       const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 0) + n.rq.h * qstride(S));
-      rqh0 = hp[0]; rqh1 = hp[1];
+      hq.m0 = hp[0]; hq.m1 = hp[1];
     }
     if (HRS && n.rs.c) {
       const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 1) + n.rs.h * qstride(S));
-      rsh0 = hp[0]; rsh1 = hp[1];
+      hs.m0 = hp[0]; hs.m1 = hp[1];
     }
     hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
     cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
@@ -511,11 +548,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (__ballot(inj)) {
       if (inj) {
         if (live && n.rq.c == 0) dcs = true;
-        else if (qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                         make_uint4(0, 0, 0, 0), lctr) && HRQ) {
-          rqh0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
-          rqh1 = make_uint4(0, 0, 0, 0);
-        }
+        else qpush<HRQ>(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                        make_uint4(0, 0, 0, 0), lctr, hq);
       }
     }
 
@@ -553,11 +587,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
           lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
         } else {
-          if (qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                      make_uint4(0, 0, 0, 0), lctr) && HRQ) {
-            rqh0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
-            rqh1 = make_uint4(0, 0, 0, 0);
-          }
+          qpush<HRQ>(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                     make_uint4(0, 0, 0, 0), lctr, hq);
         }
       }
       if (which >= 0 && !(dcs && which == 0)) {
@@ -570,9 +601,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const size_t qs = qstride(S);
         const bool hreg = which ? HRS : HRQ;
         if (hreg) {
-          const uint4 h0 = which ? rsh0 : rqh0;
+          const uint4 h0 = which ? hs.m0 : hq.m0;
           m0 = make_uint4(q.arr, h0.y, h0.z, h0.w);
-          m1 = which ? rsh1 : rqh1;
+          m1 = which ? hs.m1 : hq.m1;
+          if (which) hs.dirty = false;       // consumed: a register-only head never reaches memory
+          else hq.dirty = false;
         } else {
           const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
           m0 = sp[0];
@@ -590,8 +623,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           if (hreg) {
             const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
             const uint4 n0 = np[0], n1 = np[1];
-            if (which) { rsh0 = n0; rsh1 = n1; }
-            else { rqh0 = n0; rqh1 = n1; }
+            if (which) { hs.m0 = n0; hs.m1 = n1; }
+            else { hq.m0 = n0; hq.m1 = n1; }
           }
         }
 #else
@@ -599,8 +632,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (hreg) {
           const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
           const uint4 n0 = np[0], n1 = np[1];
-          if (which) { rsh0 = n0; rsh1 = n1; }
-          else { rqh0 = n0; rqh1 = n1; }
+          if (which) { hs.m0 = n0; hs.m1 = n1; }
+          else { hq.m0 = n0; hq.m1 = n1; }
         }
 #endif
         if (!have_w && n.role != RAFT_LEADER) {
@@ -941,13 +974,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
         const uint4 q0 = make_uint4(t + d, c0.x, sr.x, sr.y), q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
-        const bool nhd = qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
         if (which) {
+          qpush<HRS>(S, sgi, n.fault, 1, q, q0, q1, lctr, hs);
           n.rs = q;
-          if (HRS && nhd) { rsh0 = q0; rsh1 = q1; }
         } else {
+          qpush<HRQ>(S, sgi, n.fault, 0, q, q0, q1, lctr, hq);
           n.rq = q;
-          if (HRQ && nhd) { rqh0 = q0; rqh1 = q1; }
         }
         if (++copy >= (c2.y >> 16)) {
           copy = 0;
@@ -1132,6 +1164,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     S.masks[gi] = n.votes | n.keys << 16;
     S.term[gi] = n.term; S.commit[gi] = n.commit; S.len[gi] = n.len; S.deadline[gi] = n.deadline;
     S.qmeta[gi] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
+    if (HRQ && hq.dirty) {
+      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, 0) + n.rq.h * qstride(S));
+      hp[0] = make_uint4(n.rq.arr, hq.m0.y, hq.m0.z, hq.m0.w); hp[1] = hq.m1;
+    }
+    if (HRS && hs.dirty) {
+      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, 1) + n.rs.h * qstride(S));
+      hp[0] = make_uint4(n.rs.arr, hs.m0.y, hs.m0.z, hs.m0.w); hp[1] = hs.m1;
+    }
     S.req_arr[gi] = n.rq.arr; S.res_arr[gi] = n.rs.arr;
     S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
     S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
@@ -1243,10 +1283,51 @@ hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
   return hipGetLastError();
 }
 
+// scan + scatter in one workgroup: the bucket offsets live in LDS (16,384 x 4 B = 64 KiB), so
+// the scatter's position claims are LDS atomics on one CU instead of device-scope atomics that
+// cross XCDs, and the schedule costs one launch instead of two. Thread t owns buckets
+// [16t, 16t + 16); the block-wide exclusive scan of the per-thread sums is a wave scan
+// (__shfl_up) plus the 16 wave totals, parked in off[0..15] before the offsets are written.
+__global__ void __launch_bounds__(1024) sched_perm_kernel(DevSim S, uint32_t* perm) {
+  constexpr uint32_t PER = SCHED_BUCKETS / 1024;
+  __shared__ uint32_t off[SCHED_BUCKETS];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    v[i] = S.shist[t * PER + i];
+    S.shist[t * PER + i] = 0;
+    sum += v[i];
+  }
+  uint32_t inc = sum;                                 // inclusive scan inside the wave
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t x = __shfl_up(inc, d);
+    if (lane >= d) inc += x;
+  }
+  if (lane == 63) off[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t j = 0; j < w; ++j) run += off[j];
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    off[t * PER + i] = run;
+    run += v[i];
+  }
+  __syncthreads();
+  for (uint32_t c = t; c < S.C; c += 1024) perm[atomicAdd(&off[S.skey[c]], 1u)] = c;
+}
+
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st) {
+#if RS_SCHED_FUSED
+  (void)off;
+  hipLaunchKernelGGL(sched_perm_kernel, dim3(1), dim3(1024), 0, st, S, perm);
+#else
   hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(1024), 0, st, S.shist, off);
   hipLaunchKernelGGL(sched_scatter_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, off,
                      perm);
+#endif
   return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@ Usage: python scripts/ab_probe.py LIB_A LIB_B ... [--sched=0|1] [--WORKLOAD ...]
 10k-tick launch for each build on each workload, and whether the builds agree on the state."""
 import statistics
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -33,14 +34,18 @@ def main():
         for s in sims:
             s.step(10000)                               # warm up to a steady state
         times = [[] for _ in libs]
+        walls = [[] for _ in libs]
         for _ in range(rounds):
             for i, s in enumerate(sims):
+                t0 = time.perf_counter()
                 s.step(10000)
+                walls[i].append((time.perf_counter() - t0) * 1e3)
                 times[i].append(s.last_step_timing()[0])
         digests = {bytes(s.digest(0, 256)) for s in sims}
-        for lib, ts in zip(libs, times):
+        for lib, ts, ws in zip(libs, times, walls):
             print(f"{wname:6s} {Path(lib).name:28s} median {statistics.median(ts):8.3f} ms  "
-                  f"min {min(ts):8.3f} ms", flush=True)
+                  f"min {min(ts):8.3f} ms  step wall median {statistics.median(ws):8.3f} ms",
+                  flush=True)
         print(f"{wname:6s} builds agree on state: {len(digests) == 1}", flush=True)
         for s in sims:
             s.close()
