@@ -34,6 +34,9 @@ static int fail(int code, const char* fmt, const char* detail = "") {
                                       hipGetErrorString(e_));                      \
   } while (0)
 
+#ifndef RS_SCHED_RANGE
+#define RS_SCHED_RANGE 1
+#endif
 #ifndef RS_RESORT_EVERY
 #define RS_RESORT_EVERY 1
 #endif
@@ -227,25 +230,30 @@ int raft_sim_step_async(raft_sim_t* s, uint32_t n_ticks) {
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick + done;
-    rs::DevSim dl = s->d;
+    bool keyless = false;
     if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
       // pack clusters with the same next event onto the same waves for this launch: keys and
       // histogram come from the previous tick launch, or are recomputed from the state
       if (!s->d.perm || s->nlaunch % RS_RESORT_EVERY == 0) {
         if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
         HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
+#if RS_SCHED_RANGE
+        // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
+        std::swap(s->d.shist, s->soff);
+#endif
         s->d.perm = s->sperm;
-        dl.perm = s->sperm;
         s->keys_fresh = true;
       }
       // only the launch before a rebuild writes keys and histogram for it
       if ((s->nlaunch + 1) % RS_RESORT_EVERY != 0) {
-        dl.shist = nullptr;
+        keyless = true;
         s->keys_fresh = false;
       } else {
         s->keys_fresh = true;
       }
     }
+    rs::DevSim dl = s->d;
+    if (keyless) dl.shist = nullptr;
     ++s->nlaunch;
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;

@@ -377,6 +377,9 @@ constexpr size_t block_lds_bytes() {
 #ifndef RS_QRESET
 #define RS_QRESET 1
 #endif
+#ifndef RS_SCHED_RANGE
+#define RS_SCHED_RANGE 1
+#endif
 #ifndef RS_SCHED_FUSED
 #define RS_SCHED_FUSED 0
 #endif
@@ -1319,8 +1322,84 @@ __global__ void __launch_bounds__(1024) sched_perm_kernel(DevSim S, uint32_t* pe
   for (uint32_t c = t; c < S.C; c += 1024) perm[atomicAdd(&off[S.skey[c]], 1u)] = c;
 }
 
+// Scan + scatter without global atomics: block b of SCHED_RANGE_BLOCKS owns the key range
+// [b*KB, (b+1)*KB). It sums the histogram below its range (its base), scans its own KB buckets
+// into LDS offsets, then reads every cluster's key and places the clusters of its range with LDS
+// atomics. Each block reads all keys (L2-resident, 4 B per cluster), and there is one launch
+// instead of two. The histogram is double-buffered: this kernel reads S.shist and zeroes `zero`,
+// which the next tick launch fills (the host swaps the two).
+constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
+__global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* zero,
+                                                           uint32_t* perm) {
+  constexpr uint32_t KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;   // 256
+  static_assert(KB <= 1024 && KB % 64 == 0, "one thread per bucket of the range");
+  __shared__ uint32_t loff[KB];
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t k0 = blockIdx.x * KB;
+  if (t < KB) zero[k0 + t] = 0;
+  uint32_t part = 0;                                  // buckets below the range, 16 loads in flight
+#pragma unroll
+  for (uint32_t i = 0; i < SCHED_BUCKETS / 1024; ++i) {
+    const uint32_t idx = t * (SCHED_BUCKETS / 1024) + i;
+    part += idx < k0 ? S.shist[idx] : 0u;
+  }
+  const uint32_t mine = t < KB ? S.shist[k0 + t] : 0u;
+  // block sum of `part` (wave reduce, then 16 wave totals)
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d);
+  if (lane == 0) wsum[w] = part;
+  // exclusive scan of `mine` over the KB range threads (waves 0..KB/64-1)
+  uint32_t inc = mine;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t x = __shfl_up(inc, d);
+    if (lane >= d) inc += x;
+  }
+  __syncthreads();
+  uint32_t base = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) base += wsum[j];
+  __syncthreads();
+  if (t < KB && lane == 63) wsum[w] = inc;            // range-wave totals (w < KB / 64)
+  __syncthreads();
+  if (t < KB) {
+    uint32_t run = base + inc - mine;
+    for (uint32_t j = 0; j < w; ++j) run += wsum[j];
+    loff[t] = run;
+  }
+  __syncthreads();
+  // keys as 16-byte vectors, sixteen loads in flight per thread (64 keys), then the scalar tail
+  const uint32_t C4 = S.C / 4;
+  const uint4* k4 = reinterpret_cast<const uint4*>(S.skey);
+  for (uint32_t vb = t; vb < C4; vb += 16 * 1024) {
+    uint4 v[16];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t q = vb + j * 1024;
+      v[j] = q < C4 ? k4[q] : make_uint4(INF, INF, INF, INF);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t c = 4 * (vb + j * 1024);
+      const uint32_t r0 = v[j].x - k0, r1 = v[j].y - k0, r2 = v[j].z - k0, r3 = v[j].w - k0;
+      if (r0 < KB) perm[atomicAdd(&loff[r0], 1u)] = c;
+      if (r1 < KB) perm[atomicAdd(&loff[r1], 1u)] = c + 1;
+      if (r2 < KB) perm[atomicAdd(&loff[r2], 1u)] = c + 2;
+      if (r3 < KB) perm[atomicAdd(&loff[r3], 1u)] = c + 3;
+    }
+  }
+  for (uint32_t c = 4 * C4 + t; c < S.C; c += 1024) {
+    const uint32_t r = S.skey[c] - k0;
+    if (r < KB) perm[atomicAdd(&loff[r], 1u)] = c;
+  }
+}
+
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st) {
-#if RS_SCHED_FUSED
+#if RS_SCHED_RANGE
+  hipLaunchKernelGGL(sched_range_kernel, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, off,
+                     perm);
+#elif RS_SCHED_FUSED
   (void)off;
   hipLaunchKernelGGL(sched_perm_kernel, dim3(1), dim3(1024), 0, st, S, perm);
 #else
