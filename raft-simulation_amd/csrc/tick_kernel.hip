@@ -8,6 +8,12 @@
 // VALU instructions and one ballot.
 #include "device.hpp"
 
+// waves per workgroup of the tick kernel: a workgroup's LDS and slot are released only when its
+// last wave ends, so smaller workgroups refill the CU sooner when wave lifetimes differ
+#ifndef RS_WPB
+#define RS_WPB 1
+#endif
+
 namespace rs {
 
 __device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) {
@@ -369,7 +375,7 @@ constexpr int wave_lds_words() {
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + 4 * wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
+  return (PW_WORDS + RS_WPB * wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
 }
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
@@ -406,7 +412,7 @@ constexpr size_t block_lds_bytes() {
 #endif
 
 template <int N, bool TRACE, bool SPEC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
+__global__ void __launch_bounds__(64 * RS_WPB) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr int WAVE_WORDS = wave_lds_words<N, SPEC>();
@@ -428,9 +434,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #define RS_SPREAD 1
 #endif
   // With RAFT_SCHED_ALIGNED, neighbouring wave slots hold clusters with the same next event, so
-  // they are active on the same ticks. A block's four waves therefore take slots a quarter of the
-  // grid apart: the waves sharing a CU's memory pipeline are active on different ticks.
-  const uint32_t wave = (RS_SPREAD && S.perm) ? wv * gridDim.x + blockIdx.x : blockIdx.x * 4 + wv;
+  // they are active on the same ticks. A multi-wave workgroup's waves therefore take slots
+  // 1/RS_WPB of the grid apart, so waves sharing a CU are active on different ticks (with the
+  // default one-wave workgroups this is the identity).
+  const uint32_t wave = (RS_SPREAD && S.perm) ? wv * gridDim.x + blockIdx.x : blockIdx.x * RS_WPB + wv;
   const int cs = lane / N, k0 = lane - cs * N;
   const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
   const bool active = lane < CPW * N && slot < S.C;
@@ -1501,11 +1508,11 @@ void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
   constexpr int CPW = 64 / N;
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = (S.C + CPW - 1) / CPW;
-  const uint32_t blocks = (waves + 3) / 4;
+  const uint32_t blocks = (waves + RS_WPB - 1) / RS_WPB;
   if (S.TC)
-    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(blocks), dim3(64 * RS_WPB), lds, st, S, t0, nt);
   else
-    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(blocks), dim3(256), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(blocks), dim3(64 * RS_WPB), lds, st, S, t0, nt);
 }
 
 template <int N>
