@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define RAFT_SIM_ABI_VERSION 1
+#define RAFT_SIM_ABI_VERSION 2
 #define RAFT_MAX_NODES 9
 #define RAFT_MAX_INBOX 16
 
@@ -58,7 +58,9 @@ enum raft_schedule {
 };
 
 /* Replaces `-main`'s argv (core.clj:197-200), the hard-coded timeouts (core.clj:173-174) and the
- * chan buffer sizes (server.clj:37, client.clj:18). Defaults: raft_sim_default_config(). */
+ * chan buffer sizes (server.clj:37, client.clj:18). Defaults: raft_sim_default_config().
+ * Limits (-EINVAL otherwise): cluster_offset + n_clusters <= 2^32 (global ids key Philox), and
+ * nodes^2 * n_clusters < 2^31 (per-peer rows are indexed in 32 bits). */
 typedef struct raft_sim_config {
   uint32_t n_clusters;     /* clusters simulated by this handle */
   uint32_t cluster_offset; /* global id of the first one (keys Philox: shard-invariant) */
@@ -78,6 +80,19 @@ typedef struct raft_sim_config {
   uint32_t trace_cap;         /* per-node ring of `wait` events (core.clj:182-186); 0 = off */
   uint32_t trace_entry_cap;   /* per-node ring of the :entries those events carried */
   uint32_t schedule;          /* cluster->wave packing, enum raft_schedule (results identical) */
+  /* Client traffic (SIM_SPEC §4 P0, D9/D14/D15): client-sets arrive at client_ppm per tick during
+   * bursts of client_burst ticks at the start of every client_period ticks (period 0: always on),
+   * and a client follows up to client_redirects redirect-client hops (server.clj:62-63) towards the
+   * :leader-id before it abandons the command (0: a redirect ends the command). */
+  uint32_t client_period;
+  uint32_t client_burst;      /* 1..client_period when client_period > 0 */
+  uint32_t client_redirects;  /* 0..16 */
+  /* Multi-GPU inside one handle: the clusters are split into n_devices contiguous shards
+   * [n*d/G, n*(d+1)/G) (the split raftsim.dist.shard uses), shard d on HIP device
+   * (device + d) mod the visible device count, one stream each; steps run on all shards at
+   * once and raft_sim_read_counters reduces them (SUM; MIN first violation; MAX payload).
+   * 0 means 1. Results are identical for every G (Philox is keyed by the global cluster id). */
+  int32_t n_devices;
 } raft_sim_config_t;
 
 /* Canonical node record: the node map of init-node (core.clj:31-38) plus the log atom
@@ -138,13 +153,17 @@ enum raft_counter {
   RAFT_CTR_OVERFLOW, RAFT_CTR_TO_HALTED, RAFT_CTR_CLIENT_INJECTED, RAFT_CTR_HALT_IOOBE,
   RAFT_CTR_HALT_NPE, RAFT_CTR_HALT_CCE, RAFT_CTR_HALT_OVERFLOW, RAFT_CTR_ENTRIES_APPENDED,
   RAFT_CTR_ENTRIES_APPLIED, RAFT_CTR_PAYLOAD_EVICTED, RAFT_CTR_VIOL_ELECTION,
-  RAFT_CTR_VIOL_LOG, RAFT_CTR_VIOL_COMPLETE, RAFT_CTR_COUNT
+  RAFT_CTR_VIOL_LOG, RAFT_CTR_VIOL_COMPLETE,
+  RAFT_CTR_REDIRECTS,        /* client-sets re-sent along a redirect-client (server.clj:62-63) */
+  RAFT_CTR_CLIENT_ABANDONED, /* client-sets a non-leader received with no redirect hop left */
+  RAFT_CTR_COUNT
 };
 
 typedef struct raft_counters {
   uint64_t node_ticks;
   uint64_t first_violation_tick; /* UINT64_MAX when none */
-  uint64_t c[RAFT_CTR_COUNT];
+  uint64_t c[RAFT_CTR_COUNT];    /* sums */
+  uint64_t payload_max;          /* most :entries any append-entries carried (a maximum) */
 } raft_counters_t;
 
 typedef struct raft_sim raft_sim_t;
@@ -157,10 +176,12 @@ void raft_sim_default_config(raft_sim_config_t* cfg);
 int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out);
 
 /* Replaces the `(loop [node ...] (recur (wait system node)))` of -main (core.clj:202-203) for every
- * node of every cluster: advances all clusters by n_ticks (synchronous). */
+ * node of every cluster: advances all clusters by n_ticks (synchronous). A HIP failure part-way
+ * through a step leaves the state between ticks the handle cannot name, so the handle is then
+ * poisoned: every later step returns -EIO. */
 int raft_sim_step(raft_sim_t* sim, uint32_t n_ticks);
 
-/* raft_sim_step without the wait: enqueues the launches for n_ticks on the simulator's stream and
+/* raft_sim_step without the wait: enqueues the launches for n_ticks on every shard's stream and
  * returns. Reads, digests and the next step are stream-ordered after it; raft_sim_sync waits for
  * everything enqueued and makes raft_sim_last_step_timing cover those launches. Many steps
  * queued between syncs pay no host round trip per step. */
@@ -169,6 +190,12 @@ int raft_sim_sync(raft_sim_t* sim);
 
 /* Ticks simulated so far (the next tick to run). */
 uint64_t raft_sim_tick(const raft_sim_t* sim);
+
+/* Resume: set the next tick to run, for state restored through the write_* calls below (deadlines
+ * and arrivals are absolute ticks). Steps are refused (-ERANGE) once tick + n_ticks plus the
+ * longest timer or delay (max(hb, el_base + el_span, dmax)) could reach 2^32 - 1, the "never"
+ * marker, so no deadline or arrival can wrap. */
+int raft_sim_set_tick(raft_sim_t* sim, uint64_t tick);
 
 /* Replaces `(prn node)` of wait (core.clj:182-183): canonical records, N per cluster. */
 int raft_sim_read_nodes(raft_sim_t* sim, uint32_t c0, uint32_t nc, raft_node_t* out);

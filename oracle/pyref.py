@@ -70,6 +70,17 @@ def sat_tick(x):
     return x if x < M32 else M32
 
 
+def on_index(t, period, burst):
+    """Index of on-tick t among the client schedule's on-ticks (SIM_SPEC §4 P0): bursts of `burst`
+    ticks at the start of every `period`; period 0 = every tick is on."""
+    return t if period == 0 else (t // period) * burst + t % period
+
+
+def on_tick(j, period, burst):
+    """The tick of on-tick number j (inverse of on_index), saturating at 2^32-1 = never."""
+    return sat_tick(j if period == 0 else (j // burst) * period + j % burst)
+
+
 # ----------------------------------------------------------------------------------------------
 # FNV-1a-64 over u32 words (trace hash and digest, SIM_SPEC §4/§6)
 # ----------------------------------------------------------------------------------------------
@@ -317,9 +328,10 @@ def append_response_handler(message, node, stats):                   # core.clj:
     return n
 
 
-def client_set_handler(log, message, node, stats):                   # core.clj:151-160
+def client_set_handler(log, message, node, stats, redirect):         # core.clj:151-160
     if node["state"] != ":leader":
-        return node                                # redirect-client: no state change
+        redirect(node["leader-id"])                # redirect-client (server.clj:62-63)
+        return node                                # no state change
     check_capacity(log, 1)
     stats["appended_at"] = len(log.entries)
     append_string_entries(log, node["current-term"], [message["command"]])
@@ -372,7 +384,7 @@ def spec_append_entries_rpc(rpc, log, cluster, node):        # replaces core.clj
                 "entries": list(log.entries[prev:])})
 
 
-def spec_request_vote_handler(log, message, node, respond, variant):   # replaces core.clj:91-103
+def spec_request_vote_handler(log, message, node, respond, variant, stats):  # replaces core.clj:91-103
     term, cand = message["term"], message["candidate-id"]
     if term > node["current-term"]:
         node = spec_step_down(node, term)
@@ -386,6 +398,7 @@ def spec_request_vote_handler(log, message, node, respond, variant):   # replace
     if grant:
         node = dict(node)
         node["voted-for"] = cand
+        stats["rearm"] = True                      # Figure 2: granting a vote resets the timer
     return node
 
 
@@ -406,6 +419,7 @@ def spec_append_entries_handler(log, message, node, respond, stats):    # replac
     n = dict(node)
     n.update({"state": ":follower", "votes": set(), "leader-id": message["leader-id"],
               "leader-state": None})
+    stats["rearm"] = True                          # AppendEntries from the current leader
     if not consistent:
         respond(dict(response, success=False))
         return n
@@ -495,13 +509,14 @@ COUNTERS = ["ev_rv", "ev_ae", "ev_cs", "ev_vr", "ev_ar", "ev_timeout", "ev_heart
             "leaders", "sent", "delivered", "dropped", "partitioned", "duplicated", "overflow",
             "to_halted", "client_injected", "halt_ioobe", "halt_npe", "halt_cce",
             "halt_overflow", "entries_appended", "entries_applied", "payload_evicted",
-            "viol_election", "viol_log", "viol_complete"]
+            "viol_election", "viol_log", "viol_complete", "redirects", "client_abandoned"]
 
 
 def default_config(**kw):
     cfg = dict(nodes=5, log_cap=64, arena_cap=0, inbox_cap=16, seed=42, hb=3000, el_base=5000,
                el_span=5000, drop_ppm=0, dup_ppm=0, dmin=1, dmax=1, part_ppm=0, part_epoch=1000,
-               client_ppm=0, variant_flags=0, trace_cap=0)
+               client_ppm=0, variant_flags=0, trace_cap=0, client_period=0, client_burst=0,
+               client_redirects=0)
     cfg.update(kw)
     return cfg
 
@@ -542,8 +557,10 @@ class PyCluster:
         self.client_pw = client_powers(cfg["client_ppm"])
         if cfg["client_ppm"]:
             d = philox((gid, CLIENT << 8, 0, 1), self.key)
-            self.client_next = sat_tick(client_gap(d[0], self.client_pw))
+            self.client_next = on_tick(client_gap(d[0], self.client_pw), cfg["client_period"],
+                                       cfg["client_burst"])
         self.cnt = {k: 0 for k in COUNTERS}
+        self.payload_max = 0
         self.first_violation = None
         self.deadline = {}
         for i in ids:
@@ -577,6 +594,12 @@ class PyCluster:
     def transmit(self, s, r, t, msg, outbox, sides):
         """P2 fault draws for one emitted message (SIM_SPEC §4 P2)."""
         cfg = self.cfg
+        if msg["type"] == "client-set":            # a followed redirect: the client channel
+            self.cnt["redirects"] += 1
+            outbox.setdefault(r, []).append((s, [(t + 1, msg)]))
+            return
+        if msg["type"] == "append-entries":
+            self.payload_max = max(self.payload_max, len(msg["entries"]))
         self.cnt["sent"] += 1
         if sides is not None and ((sides >> s) & 1) != ((sides >> r) & 1):
             self.cnt["partitioned"] += 1
@@ -604,9 +627,11 @@ class PyCluster:
             d = philox((self.gid, CLIENT << 8, self.client_count, 0), self.key)
             target = 1 + ((d[1] * N) >> 32)
             self.cnt["client_injected"] += 1
-            self.insert(target, t, {"type": "client-set", "command": d[2]})
+            self.insert(target, t, {"type": "client-set", "command": d[2], "hops": 0})
             self.client_count = (self.client_count + 1) & M32
-            self.client_next = sat_tick(t + 1 + client_gap(d[3], self.client_pw))
+            P, B = cfg["client_period"], cfg["client_burst"]
+            self.client_next = on_tick(on_index(t, P, B) + 1 + client_gap(d[3], self.client_pw),
+                                       P, B)
         sides = self.partition_sides(t)
         outbox = {}
         elected, appended, match_changed = {}, {}, set()
@@ -640,8 +665,19 @@ class PyCluster:
             def respond(body, sends=sends, msg=msg):
                 sends.append((msg_src(msg), body))
 
+            def redirect(leader_id, sends=sends, msg=msg, i=i, w=w):
+                # redirect-client (server.clj:62-63) to the :leader-id, or to (rand-nth cluster)
+                # when it is nil (core.clj:153-155); the client follows it (SIM_SPEC §4 D15)
+                peers = self.cluster[i]
+                target = leader_id if leader_id is not None else peers[(w[2] * len(peers)) >> 32]
+                hops = msg.get("hops", 0)
+                if hops < cfg["client_redirects"]:
+                    sends.append((target, dict(msg, hops=hops + 1)))
+                else:
+                    self.cnt["client_abandoned"] += 1
+
             stats = {"entries_appended": 0, "entries_applied": 0, "appended_at": None,
-                     "elected": False, "match_changed": False, "written": []}
+                     "elected": False, "match_changed": False, "written": [], "rearm": False}
             cluster = self.cluster[i]
             spec = bool(cfg["variant_flags"] & SPEC)
             try:
@@ -664,11 +700,11 @@ class PyCluster:
                     ev = TYPE_CODE[msg["type"]]
                     if ev == 1:
                         new = spec_request_vote_handler(log, msg, node, respond,
-                                                        cfg["variant_flags"])
+                                                        cfg["variant_flags"], stats)
                     elif ev == 2:
                         new = spec_append_entries_handler(log, msg, node, respond, stats)
                     elif ev == 3:
-                        new = client_set_handler(log, msg, node, stats)
+                        new = client_set_handler(log, msg, node, stats, redirect)
                     elif ev == 4:
                         new = spec_vote_response_handler(rpc, log, cluster, msg, node, stats)
                     else:
@@ -680,7 +716,7 @@ class PyCluster:
                     elif ev == 2:
                         new = append_entries_handler(log, msg, node, respond, stats)
                     elif ev == 3:
-                        new = client_set_handler(log, msg, node, stats)
+                        new = client_set_handler(log, msg, node, stats, redirect)
                     elif ev == 4:
                         new = vote_response_handler(rpc, log, cluster, msg, node, stats)
                     else:
@@ -703,10 +739,14 @@ class PyCluster:
                 elected[i] = new["current-term"]
             if stats["match_changed"]:
                 match_changed.add(i)
-            if new["state"] == ":leader":
-                self.deadline[i] = t + cfg["hb"]
-            else:
-                self.deadline[i] = t + cfg["el_base"] + ((w[1] * cfg["el_span"]) >> 32)
+            election = t + cfg["el_base"] + ((w[1] * cfg["el_span"]) >> 32)
+            if not spec:                                     # D4: every event re-arms the timer
+                self.deadline[i] = t + cfg["hb"] if new["state"] == ":leader" else election
+            elif new["state"] == ":leader":                  # SIM_SPEC §8 (Raft §5.2 timers)
+                if ev == 7 or stats["elected"]:
+                    self.deadline[i] = t + cfg["hb"]
+            elif ev == 6 or stats["rearm"] or node["state"] == ":leader":
+                self.deadline[i] = election
             self.trace[i] = fnv(self.trace[i], self._trace_words(t, ev, msg, new, 0))
             for p, m in sends:
                 self.transmit(i, p, t, m, outbox, sides)
@@ -831,7 +871,7 @@ def encode_msg(arrival, m):
     else:
         e = None
         if code == 3:
-            a = m["command"]
+            a, b = m["command"], m.get("hops", 0)
         elif code == 4:
             term, flag = m["term"], int(m["vote-granted"])
         else:

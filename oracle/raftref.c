@@ -6,6 +6,9 @@
  */
 #include "raftref.h"
 
+typedef struct shard shard_t;
+static void sh_destroy(shard_t* s);
+
 #include <errno.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -34,7 +37,7 @@ void raft_ref_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
+static void draw(const shard_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
                  uint32_t w[4]);
 static uint32_t ppm(uint32_t w) { return (uint32_t)(((uint64_t)w * 1000000u) >> 32); }
 
@@ -56,13 +59,22 @@ static uint64_t client_gap(uint32_t w, const uint64_t pw[32]) {
 
 static uint32_t sat_tick(uint64_t x) { return x < 0xFFFFFFFFull ? (uint32_t)x : 0xFFFFFFFFu; }
 
+/* Client schedule (SIM_SPEC §4 P0): bursts of B on-ticks at the start of every period P (P = 0:
+ * every tick is on). on_index numbers the on-ticks, on_tick maps a number back to its tick. */
+static uint64_t on_index(uint64_t t, uint32_t P, uint32_t B) {
+  return P ? (t / P) * B + t % P : t;
+}
+static uint32_t on_tick(uint64_t j, uint32_t P, uint32_t B) {
+  return sat_tick(P ? (j / B) * P + j % B : j);
+}
+
 /* ---------------------------------------------------------------- FNV-1a-64 over u32 words */
 #define FNV_OFFSET 0xCBF29CE484222325ull
 #define FNV_PRIME 0x100000001B3ull
 static uint64_t fnv(uint64_t h, uint32_t w) { return (h ^ w) * FNV_PRIME; }
 
 /* ---------------------------------------------------------------- simulator state */
-struct raft_ref {
+struct shard {
   raft_sim_config_t cfg;
   uint32_t N, Q, L, A, C;
   uint32_t key[2];
@@ -80,10 +92,11 @@ struct raft_ref {
   uint32_t TC, TE;
   raft_counters_t ctr;
   int threads;
+  int idle_skip;   /* jump over ticks at which no node of a cluster can act (same results) */
   uint64_t client_pw[32];
 };
 
-static void draw(const raft_ref_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
+static void draw(const shard_t* s, uint32_t g, uint32_t nodep, uint32_t t, uint32_t x,
                  uint32_t w[4]) {
   uint32_t ctr[4] = {g, nodep, t, x};
   raft_ref_philox(ctr, s->key, w);
@@ -93,13 +106,13 @@ void raft_ref_default_config(raft_sim_config_t* c) {
   memset(c, 0, sizeof *c);
   c->n_clusters = 1; c->nodes = 5; c->log_cap = 64; c->inbox_cap = 16; c->seed = 42;
   c->hb = 3000; c->el_base = 5000; c->el_span = 5000; c->dmin = 1; c->dmax = 1;
-  c->part_epoch = 1000;
+  c->part_epoch = 1000; c->n_devices = 1;
 }
 
-static raft_msg_t* qslot(raft_ref_t* s, uint32_t gi, int which) {
+static raft_msg_t* qslot(shard_t* s, uint32_t gi, int which) {
   return s->q + ((size_t)gi * 2 + which) * s->Q;
 }
-static raft_entry_t* arena_of(raft_ref_t* s, uint32_t gi) { return s->arena + (size_t)gi * s->A; }
+static raft_entry_t* arena_of(shard_t* s, uint32_t gi) { return s->arena + (size_t)gi * s->A; }
 
 static int validate_cfg(const raft_sim_config_t* c) {
   if (c->nodes < 2 || c->nodes > RAFT_MAX_NODES) return fail(-EINVAL, "nodes must be 2..9");
@@ -116,14 +129,22 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->variant_flags & ~3u) return fail(-EINVAL, "variant_flags: only bits 0-1 are defined");
   if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
     return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
+  if ((uint64_t)c->cluster_offset + c->n_clusters > (1ull << 32))
+    return fail(-EINVAL, "cluster_offset + n_clusters must be <= 2^32");
+  if ((uint64_t)c->nodes * c->nodes * c->n_clusters >= (1ull << 31))
+    return fail(-EINVAL, "nodes^2 * n_clusters must be < 2^31");
+  if (c->client_period && (c->client_burst < 1 || c->client_burst > c->client_period))
+    return fail(-EINVAL, "client_burst must be 1..client_period");
+  if (c->client_redirects > 16) return fail(-EINVAL, "client_redirects <= 16");
+  if (c->n_devices < 0 || c->n_devices > 64) return fail(-EINVAL, "n_devices 0..64");
   return 0;
 }
 
-int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
+static int sh_create(const raft_sim_config_t* cfg, shard_t** out) {
   if (!cfg || !out) return fail(-EINVAL, "null argument");
   int rc = validate_cfg(cfg);
   if (rc) return rc;
-  raft_ref_t* s = (raft_ref_t*)calloc(1, sizeof *s);
+  shard_t* s = (shard_t*)calloc(1, sizeof *s);
   if (!s) return fail(-ENOMEM, "oom");
   s->cfg = *cfg;
   s->N = cfg->nodes; s->Q = cfg->inbox_cap; s->L = cfg->log_cap; s->C = cfg->n_clusters;
@@ -143,7 +164,7 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
   s->tent = (raft_entry_t*)calloc(nn * (s->TE ? s->TE : 1), sizeof(raft_entry_t));
   s->tecount = (uint32_t*)calloc(nn, sizeof(uint32_t));
   if (!s->nodes || !s->q || !s->arena || !s->cl || !s->stream || !s->tr || !s->tcount || !s->tent ||
-      !s->tecount) { raft_ref_destroy(s); return fail(-ENOMEM, "oom"); }
+      !s->tecount) { sh_destroy(s); return fail(-ENOMEM, "oom"); }
   client_powers(cfg->client_ppm, s->client_pw);
   for (uint32_t c = 0; c < s->C; ++c) {
     uint32_t g = cfg->cluster_offset + c;
@@ -151,7 +172,8 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
     if (cfg->client_ppm) {
       uint32_t d[4];
       draw(s, g, P_CLIENT << 8, 0, 1, d);
-      s->cl[c].client_next = sat_tick(client_gap(d[0], s->client_pw));
+      s->cl[c].client_next = on_tick(client_gap(d[0], s->client_pw), cfg->client_period,
+                                     cfg->client_burst);
     }
     for (uint32_t k = 0; k < s->N; ++k) {
       raft_node_t* n = &s->nodes[(size_t)c * s->N + k];
@@ -168,26 +190,25 @@ int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
   return 0;
 }
 
-int raft_ref_set_threads(raft_ref_t* s, int threads) {
+static int sh_set_threads(shard_t* s, int threads) {
   if (!s || threads < 1 || threads > 1024) return fail(-EINVAL, "threads 1..1024");
   s->threads = threads;
   return 0;
 }
 
-void raft_ref_destroy(raft_ref_t* s) {
+static void sh_destroy(shard_t* s) {
   if (!s) return;
   free(s->nodes); free(s->q); free(s->arena); free(s->cl); free(s->stream);
   free(s->tr); free(s->tcount); free(s->tent); free(s->tecount); free(s);
 }
 
-uint64_t raft_ref_tick(const raft_ref_t* s) { return s ? s->tick : 0; }
-int raft_ref_step_async(raft_ref_t* s, uint32_t n_ticks) { return raft_ref_step(s, n_ticks); }
-int raft_ref_sync(raft_ref_t* s) { return s ? 0 : fail(-EINVAL, "null sim"); }
+uint64_t shard_tick(const shard_t* s) { return s ? s->tick : 0; }
 
 /* ---------------------------------------------------------------- per-cluster tick */
 typedef struct {
   uint64_t c[RAFT_CTR_COUNT];
   uint64_t first_violation;
+  uint64_t payload_max;
 } local_ctr_t;
 
 typedef struct { int n; uint32_t arr[2]; raft_msg_t m; } cell_t;
@@ -200,7 +221,7 @@ typedef struct {
 } plan_t;
 
 typedef struct {
-  raft_ref_t* s;
+  shard_t* s;
   uint32_t c, g, t, N;
   raft_node_t* nodes;
   local_ctr_t* lc;
@@ -294,7 +315,7 @@ static void plan_append(tick_ctx_t* x, raft_node_t* nn, plan_t* pl, uint32_t m) 
 }
 
 static void queue_insert(tick_ctx_t* x, uint32_t k, const raft_msg_t* m) {
-  raft_ref_t* s = x->s;
+  shard_t* s = x->s;
   raft_node_t* n = &x->nodes[k];
   uint32_t type = m->hdr & 7;
   int which = type <= RAFT_MSG_CLIENT_SET ? 0 : 1;
@@ -312,6 +333,14 @@ static void queue_insert(tick_ctx_t* x, uint32_t k, const raft_msg_t* m) {
 /* Network (SIM_SPEC §4 P2): faults for one emitted message s->r. */
 static void transmit(tick_ctx_t* x, uint32_t s_id, uint32_t r_id, const raft_msg_t* m) {
   const raft_sim_config_t* cfg = &x->s->cfg;
+  cell_t* rc = &x->cell[s_id - 1][r_id - 1];
+  if ((m->hdr & 7) == RAFT_MSG_CLIENT_SET) {  /* a followed redirect: client channel, 1 tick */
+    x->lc->c[RAFT_CTR_REDIRECTS]++;
+    rc->m = *m; rc->n = 1; rc->arr[0] = x->t + 1;
+    return;
+  }
+  if ((m->hdr & 7) == RAFT_MSG_APPEND_ENTRIES && (m->hdr >> 16) > x->lc->payload_max)
+    x->lc->payload_max = m->hdr >> 16;
   x->lc->c[RAFT_CTR_SENT]++;
   if (x->part && (((x->sides >> s_id) ^ (x->sides >> r_id)) & 1)) {
     x->lc->c[RAFT_CTR_PARTITIONED]++;
@@ -334,6 +363,27 @@ static void transmit(tick_ctx_t* x, uint32_t s_id, uint32_t r_id, const raft_msg
     cl->n = 2;
     cl->arr[1] = x->t + cfg->dmin + (uint32_t)(((uint64_t)w[3] * span) >> 32);
   }
+}
+
+/* redirect-client (server.clj:62-63) of a non-leader's client-set-handler (core.clj:152-155): to
+ * the :leader-id, or to (rand-nth cluster) when it is nil -- peer index w2*(N-1)>>32 of the peers
+ * ascending, w being the node's EVENT draw. The client follows it while the message has hops left
+ * (SIM_SPEC §4 D15); otherwise it abandons the command. No state change. */
+static void redirect(tick_ctx_t* x, uint32_t k, const raft_msg_t* m, const uint32_t w[4],
+                     emit_t* em, int* ne) {
+  uint32_t target = x->nodes[k].leader_id;
+  if (!target) {
+    uint32_t i = (uint32_t)(((uint64_t)w[2] * (x->N - 1)) >> 32);
+    target = i + 1 < k + 1 ? i + 1 : i + 2;
+  }
+  if (m->b >= x->s->cfg.client_redirects) {
+    x->lc->c[RAFT_CTR_CLIENT_ABANDONED]++;
+    return;
+  }
+  raft_msg_t r = *m;
+  r.arrival = 0;
+  r.b = m->b + 1;
+  em[*ne].dst = target; em[*ne].m = r; (*ne)++;
 }
 
 static uint64_t trace(uint64_t h, uint32_t t, uint32_t ev, uint32_t src, uint32_t mterm,
@@ -382,7 +432,7 @@ static void spec_ae_broadcast(tick_ctx_t* x, uint32_t k, const raft_node_t* nn, 
   }
 }
 
-static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc) {
+static void step_cluster(shard_t* s, uint32_t c, uint32_t t, local_ctr_t* lc) {
   const raft_sim_config_t* cfg = &s->cfg;
   tick_ctx_t X;
   tick_ctx_t* x = &X;
@@ -403,7 +453,9 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
     lc->c[RAFT_CTR_CLIENT_INJECTED]++;
     queue_insert(x, target - 1, &m);
     cr->client_count += 1;
-    cr->client_next = sat_tick((uint64_t)t + 1 + client_gap(d[3], s->client_pw));
+    cr->client_next = on_tick(on_index(t, cfg->client_period, cfg->client_burst) + 1 +
+                                  client_gap(d[3], s->client_pw),
+                              cfg->client_period, cfg->client_burst);
   }
   x->part = 0; x->sides = 0;
   if (cfg->part_ppm) {
@@ -471,7 +523,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
     }
     raft_node_t nn = *n;
     emit_t em[RAFT_MAX_NODES];
-    int ne = 0, fault = 0, elect = 0, mchg = 0;
+    int ne = 0, fault = 0, elect = 0, mchg = 0, rearm = 0;
     uint32_t ev, msrc = 0, mterm = 0;
     uint64_t appended = 0, applied = 0;
     uint32_t type = m.hdr & 7, src = (m.hdr >> 3) & 15, flag = (m.hdr >> 7) & 1;
@@ -518,7 +570,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
                    (mt == lt && m.a >= n->log_len);
           int grant = m.term == nn.current_term &&
                       (nn.voted_for == 0 || nn.voted_for == src) && up;
-          if (grant) nn.voted_for = (uint8_t)src;
+          if (grant) { nn.voted_for = (uint8_t)src; rearm = 1; }   /* Figure 2 timer reset */
           r.term = nn.current_term;
           r.hdr = hdr(RAFT_MSG_VOTE_RESPONSE, id, (uint32_t)grant, 0, 0);
           em[ne].dst = src; em[ne].m = r; ne++;
@@ -529,6 +581,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
           r.hdr = hdr(RAFT_MSG_APPEND_RESPONSE, id, 0, 0, 0);
           if (m.term < nn.current_term) { em[ne].dst = src; em[ne].m = r; ne++; break; }
           nn.role = RAFT_FOLLOWER; nn.votes = 0; nn.leader_id = (uint8_t)src;
+          rearm = 1;                                 /* AppendEntries from the current leader */
           if (nn.ls_present) {
             nn.ls_present = 0; nn.ls_keys = 0;
             memset(nn.next_index, 0, sizeof nn.next_index);
@@ -576,7 +629,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
           break;
         }
         case RAFT_MSG_CLIENT_SET: {                     /* as client-set-handler 151-160 */
-          if (n->role != RAFT_LEADER) break;
+          if (n->role != RAFT_LEADER) { redirect(x, k, &m, w, em, &ne); break; }
           plan[k].kind = PLAN_ENTRY;
           plan[k].entry.term = n->current_term; plan[k].entry.val = m.a;
           plan_append(x, &nn, &plan[k], 1);
@@ -701,7 +754,7 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
           break;
         }
         case RAFT_MSG_CLIENT_SET: {                          /* client-set-handler 151-160 */
-          if (n->role != RAFT_LEADER) break;                  /* redirect-client: no state */
+          if (n->role != RAFT_LEADER) { redirect(x, k, &m, w, em, &ne); break; }
           if (n->log_len + 1 > s->L) { fault = RAFT_FAULT_OVERFLOW; break; }
           plan[k].kind = PLAN_ENTRY;
           plan[k].entry.term = n->current_term; plan[k].entry.val = m.a;
@@ -768,10 +821,15 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
       appended_at[k] = -1;
       continue;
     }
-    /* generate-timeout (core.clj:171-174) for the next wait */
-    nn.deadline = nn.role == RAFT_LEADER
-                      ? t + cfg->hb
-                      : t + cfg->el_base + (uint32_t)(((uint64_t)w[1] * cfg->el_span) >> 32);
+    /* generate-timeout (core.clj:171-174) for the next wait (D4); Spec-Raft: Raft's timers */
+    const uint32_t election = t + cfg->el_base + (uint32_t)(((uint64_t)w[1] * cfg->el_span) >> 32);
+    if (!spec)
+      nn.deadline = nn.role == RAFT_LEADER ? t + cfg->hb : election;
+    else if (nn.role == RAFT_LEADER) {
+      if (ev == 7 || elect) nn.deadline = t + cfg->hb;
+    } else if (ev == 6 || rearm || n->role == RAFT_LEADER) {
+      nn.deadline = election;
+    }
     nn.trace_hash = trace(n->trace_hash, t, ev, msrc, mterm, &nn, 0);
     *n = nn;
     lc->c[RAFT_CTR_EV_RV + ev - 1]++;
@@ -920,23 +978,49 @@ static void step_cluster(raft_ref_t* s, uint32_t c, uint32_t t, local_ctr_t* lc)
 
 /* ---------------------------------------------------------------- stepping (pmap over chunks) */
 typedef struct {
-  raft_ref_t* s;
+  shard_t* s;
   uint32_t c0, c1, t0, n;
   local_ctr_t lc;
 } job_t;
+
+/* The earliest tick >= t at which cluster c can do anything: a running node's deadline or queue
+ * head, or the next client-set (SIM_SPEC §4: nothing else is keyed to a tick). */
+static uint32_t next_event(const shard_t* s, uint32_t c) {
+  uint32_t m = s->cl[c].client_next;
+  for (uint32_t k = 0; k < s->N; ++k) {
+    const raft_node_t* n = &s->nodes[(size_t)c * s->N + k];
+    if (n->fault) continue;
+    if (n->deadline < m) m = n->deadline;
+    const raft_msg_t* rq = s->q + ((size_t)(c * s->N + k) * 2) * s->Q;
+    const raft_msg_t* rs = rq + s->Q;
+    if (n->req_count && rq[0].arrival < m) m = rq[0].arrival;
+    if (n->res_count && rs[0].arrival < m) m = rs[0].arrival;
+  }
+  return m;
+}
 
 static void* run_job(void* arg) {
   job_t* j = (job_t*)arg;
   memset(&j->lc, 0, sizeof j->lc);
   j->lc.first_violation = UINT64_MAX;
-  for (uint32_t c = j->c0; c < j->c1; ++c)
-    for (uint32_t i = 0; i < j->n; ++i) step_cluster(j->s, c, j->t0 + i, &j->lc);
+  const uint64_t end = (uint64_t)j->t0 + j->n;
+  for (uint32_t c = j->c0; c < j->c1; ++c) {
+    if (!j->s->idle_skip) {
+      for (uint32_t i = 0; i < j->n; ++i) step_cluster(j->s, c, j->t0 + i, &j->lc);
+      continue;
+    }
+    for (uint64_t t = j->t0; t < end;) {     /* discrete-event skipping, tick-exact */
+      const uint32_t nx = next_event(j->s, c);
+      if (nx > t) t = nx < end ? nx : end;
+      if (t == end) break;
+      step_cluster(j->s, c, (uint32_t)t, &j->lc);
+      ++t;
+    }
+  }
   return NULL;
 }
 
-int raft_ref_step(raft_ref_t* s, uint32_t n_ticks) {
-  if (!s) return fail(-EINVAL, "null sim");
-  if (s->tick + n_ticks > 0xFFFFFFFFull) return fail(-EINVAL, "tick counter would exceed 2^32");
+static int sh_step(shard_t* s, uint32_t n_ticks) {
   int T = s->threads;
   if ((uint32_t)T > s->C) T = (int)s->C;
   job_t* jobs = (job_t*)calloc((size_t)T, sizeof *jobs);
@@ -957,6 +1041,7 @@ int raft_ref_step(raft_ref_t* s, uint32_t n_ticks) {
     for (int k = 0; k < RAFT_CTR_COUNT; ++k) s->ctr.c[k] += jobs[i].lc.c[k];
     if (jobs[i].lc.first_violation < s->ctr.first_violation_tick)
       s->ctr.first_violation_tick = jobs[i].lc.first_violation;
+    if (jobs[i].lc.payload_max > s->ctr.payload_max) s->ctr.payload_max = jobs[i].lc.payload_max;
   }
   s->ctr.node_ticks += (uint64_t)s->C * s->N * n_ticks;
   s->tick += n_ticks;
@@ -965,25 +1050,25 @@ int raft_ref_step(raft_ref_t* s, uint32_t n_ticks) {
 }
 
 /* ---------------------------------------------------------------- state access */
-static int check_range(raft_ref_t* s, uint32_t c0, uint32_t nc) {
+static int check_range(shard_t* s, uint32_t c0, uint32_t nc) {
   if (!s) return fail(-EINVAL, "null sim");
   if ((uint64_t)c0 + nc > s->C) return fail(-EINVAL, "cluster range out of bounds");
   return 0;
 }
-static int check_node(raft_ref_t* s, uint32_t cluster, uint32_t id) {
+static int check_node(shard_t* s, uint32_t cluster, uint32_t id) {
   if (!s) return fail(-EINVAL, "null sim");
   if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
   return 0;
 }
 
-int raft_ref_read_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
+static int sh_read_nodes(shard_t* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   memcpy(out, s->nodes + (size_t)c0 * s->N, (size_t)nc * s->N * sizeof(raft_node_t));
   return 0;
 }
 
-int raft_ref_write_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+static int sh_write_nodes(shard_t* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   const uint32_t N = s->N, all = ((1u << (N + 1)) - 1) & ~1u;
@@ -1009,7 +1094,7 @@ int raft_ref_write_nodes(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_nod
   return 0;
 }
 
-int raft_ref_read_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+static int sh_read_queue(shard_t* s, uint32_t cluster, uint32_t id, uint32_t which,
                         raft_msg_t* out, uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1021,7 +1106,7 @@ int raft_ref_read_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t w
   return (int)cnt;
 }
 
-int raft_ref_write_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+static int sh_write_queue(shard_t* s, uint32_t cluster, uint32_t id, uint32_t which,
                          const raft_msg_t* in, uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1042,7 +1127,7 @@ int raft_ref_write_queue(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t 
   return 0;
 }
 
-int raft_ref_read_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
+static int sh_read_arena(shard_t* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
                         uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1051,7 +1136,7 @@ int raft_ref_read_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, raft_entry
   return (int)s->A;
 }
 
-int raft_ref_write_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+static int sh_write_arena(shard_t* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
                          uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1062,7 +1147,7 @@ int raft_ref_write_arena(raft_ref_t* s, uint32_t cluster, uint32_t id, const raf
   return 0;
 }
 
-int raft_ref_read_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t* out,
+static int sh_read_commit_stream(shard_t* s, uint32_t cluster, uint32_t id, uint32_t* out,
                                 uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1074,7 +1159,7 @@ int raft_ref_read_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, ui
   return (int)kept;
 }
 
-int raft_ref_write_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, const uint32_t* in,
+static int sh_write_commit_stream(shard_t* s, uint32_t cluster, uint32_t id, const uint32_t* in,
                                  uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1085,7 +1170,7 @@ int raft_ref_write_commit_stream(raft_ref_t* s, uint32_t cluster, uint32_t id, c
   return 0;
 }
 
-int raft_ref_read_trace(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+static int sh_read_trace(shard_t* s, uint32_t cluster, uint32_t id, uint32_t first,
                         raft_trace_event_t* out, uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1097,7 +1182,7 @@ int raft_ref_read_trace(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t f
   return (int)n;
 }
 
-int raft_ref_read_trace_entries(raft_ref_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+static int sh_read_trace_entries(shard_t* s, uint32_t cluster, uint32_t id, uint32_t first,
                                 raft_entry_t* out, uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -1111,14 +1196,14 @@ int raft_ref_read_trace_entries(raft_ref_t* s, uint32_t cluster, uint32_t id, ui
   return (int)n;
 }
 
-int raft_ref_read_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
+static int sh_read_clusters(shard_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   memcpy(out, s->cl + c0, nc * sizeof *out);
   return 0;
 }
 
-int raft_ref_write_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
+static int sh_write_clusters(shard_t* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   memcpy(s->cl + c0, in, nc * sizeof *in);
@@ -1126,13 +1211,13 @@ int raft_ref_write_clusters(raft_ref_t* s, uint32_t c0, uint32_t nc, const raft_
   return 0;
 }
 
-int raft_ref_read_counters(raft_ref_t* s, raft_counters_t* out) {
+static int sh_read_counters(shard_t* s, raft_counters_t* out) {
   if (!s || !out) return fail(-EINVAL, "null argument");
   *out = s->ctr;
   return 0;
 }
 
-int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
+static int sh_digest(shard_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   const uint32_t N = s->N;
@@ -1202,3 +1287,203 @@ int raft_ref_digest(raft_ref_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
 }
 
 int raft_ref_abi_version(void) { return RAFT_SIM_ABI_VERSION; }
+
+/* ---------------------------------------------------------------- the handle: G shards
+ * Mirrors the product's n_devices (include/raftsim.h): clusters split into contiguous shards
+ * [C*d/G, C*(d+1)/G), each simulated independently with its global cluster ids; calls addressed
+ * to clusters are routed to the shard that owns them, counters are reduced (SUM, MIN, MAX). */
+struct raft_ref {
+  raft_sim_config_t cfg;
+  int G;
+  shard_t* sh[64];
+  uint32_t lo[65];   /* shard d owns local clusters [lo[d], lo[d+1]) */
+  uint64_t tick;
+};
+
+int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out) {
+  if (!cfg || !out) return fail(-EINVAL, "null argument");
+  int rc = validate_cfg(cfg);
+  if (rc) return rc;
+  raft_ref_t* r = (raft_ref_t*)calloc(1, sizeof *r);
+  if (!r) return fail(-ENOMEM, "oom");
+  r->cfg = *cfg;
+  r->G = cfg->n_devices > 1 ? cfg->n_devices : 1;
+  if ((uint32_t)r->G > cfg->n_clusters) r->G = (int)cfg->n_clusters;
+  for (int d = 0; d <= r->G; ++d) r->lo[d] = (uint32_t)((uint64_t)cfg->n_clusters * d / r->G);
+  for (int d = 0; d < r->G; ++d) {
+    raft_sim_config_t c = *cfg;
+    c.n_clusters = r->lo[d + 1] - r->lo[d];
+    c.cluster_offset = cfg->cluster_offset + r->lo[d];
+    c.n_devices = 1;
+    if ((rc = sh_create(&c, &r->sh[d]))) { raft_ref_destroy(r); return rc; }
+  }
+  *out = r;
+  return 0;
+}
+
+void raft_ref_destroy(raft_ref_t* r) {
+  if (!r) return;
+  for (int d = 0; d < r->G; ++d) sh_destroy(r->sh[d]);
+  free(r);
+}
+
+int raft_ref_set_idle_skip(raft_ref_t* r, int on) {
+  if (!r) return fail(-EINVAL, "null sim");
+  for (int d = 0; d < r->G; ++d) r->sh[d]->idle_skip = on != 0;
+  return 0;
+}
+
+int raft_ref_set_threads(raft_ref_t* r, int threads) {
+  if (!r) return fail(-EINVAL, "null sim");
+  for (int d = 0; d < r->G; ++d) {
+    int rc = sh_set_threads(r->sh[d], threads);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+/* SIM_SPEC §4 D1: no deadline or arrival may reach 2^32-1 (the "never" marker) */
+static int horizon_ok(const raft_sim_config_t* c, uint64_t tick, uint32_t n) {
+  uint64_t longest = c->hb;
+  if ((uint64_t)c->el_base + c->el_span > longest) longest = (uint64_t)c->el_base + c->el_span;
+  if (c->dmax > longest) longest = c->dmax;
+  return tick + n + longest < 0xFFFFFFFFull;
+}
+
+int raft_ref_step(raft_ref_t* r, uint32_t n_ticks) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if (!horizon_ok(&r->cfg, r->tick, n_ticks))
+    return fail(-ERANGE, "tick + n_ticks + the longest timer would reach 2^32-1");
+  for (int d = 0; d < r->G; ++d) {
+    int rc = sh_step(r->sh[d], n_ticks);
+    if (rc) return rc;
+  }
+  r->tick += n_ticks;
+  return 0;
+}
+int raft_ref_step_async(raft_ref_t* r, uint32_t n_ticks) { return raft_ref_step(r, n_ticks); }
+int raft_ref_sync(raft_ref_t* r) { return r ? 0 : fail(-EINVAL, "null sim"); }
+uint64_t raft_ref_tick(const raft_ref_t* r) { return r ? r->tick : 0; }
+
+int raft_ref_set_tick(raft_ref_t* r, uint64_t tick) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if (!horizon_ok(&r->cfg, tick, 0)) return fail(-ERANGE, "tick beyond the 32-bit horizon");
+  r->tick = tick;
+  for (int d = 0; d < r->G; ++d) r->sh[d]->tick = tick;
+  return 0;
+}
+
+/* the shard owning local cluster c, and c's index inside it */
+static shard_t* owner(raft_ref_t* r, uint32_t c, uint32_t* lc) {
+  int d = 0;
+  while (d + 1 < r->G && c >= r->lo[d + 1]) ++d;
+  *lc = c - r->lo[d];
+  return r->sh[d];
+}
+
+static int check_span(raft_ref_t* r, uint32_t c0, uint32_t nc) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if ((uint64_t)c0 + nc > r->cfg.n_clusters) return fail(-EINVAL, "cluster range out of bounds");
+  return 0;
+}
+
+/* Apply `fn` to the pieces of [c0, c0+nc) per shard; `stride` elements per cluster in `buf`. */
+#define FOR_PIECES(r, c0, nc, BODY)                                                     \
+  for (uint32_t done = 0; done < (nc);) {                                               \
+    uint32_t lc_;                                                                       \
+    shard_t* sh_ = owner((r), (c0) + done, &lc_);                                        \
+    uint32_t n_ = sh_->C - lc_;                                                          \
+    if (n_ > (nc) - done) n_ = (nc) - done;                                              \
+    BODY;                                                                               \
+    done += n_;                                                                         \
+  }
+
+int raft_ref_read_nodes(raft_ref_t* r, uint32_t c0, uint32_t nc, raft_node_t* out) {
+  int rc = check_span(r, c0, nc);
+  if (rc) return rc;
+  FOR_PIECES(r, c0, nc, if ((rc = sh_read_nodes(sh_, lc_, n_, out + (size_t)done * r->cfg.nodes))) return rc)
+  return 0;
+}
+int raft_ref_write_nodes(raft_ref_t* r, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+  int rc = check_span(r, c0, nc);
+  if (rc) return rc;
+  FOR_PIECES(r, c0, nc, if ((rc = sh_write_nodes(sh_, lc_, n_, in + (size_t)done * r->cfg.nodes))) return rc)
+  return 0;
+}
+int raft_ref_read_clusters(raft_ref_t* r, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
+  int rc = check_span(r, c0, nc);
+  if (rc) return rc;
+  FOR_PIECES(r, c0, nc, if ((rc = sh_read_clusters(sh_, lc_, n_, out + done))) return rc)
+  return 0;
+}
+int raft_ref_write_clusters(raft_ref_t* r, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
+  int rc = check_span(r, c0, nc);
+  if (rc) return rc;
+  FOR_PIECES(r, c0, nc, if ((rc = sh_write_clusters(sh_, lc_, n_, in + done))) return rc)
+  return 0;
+}
+int raft_ref_digest(raft_ref_t* r, uint32_t c0, uint32_t nc, uint64_t* out) {
+  int rc = check_span(r, c0, nc);
+  if (rc) return rc;
+  FOR_PIECES(r, c0, nc, if ((rc = sh_digest(sh_, lc_, n_, out + done))) return rc)
+  return 0;
+}
+
+static shard_t* node_owner(raft_ref_t* r, uint32_t cluster, uint32_t* lc) {
+  if (!r || cluster >= r->cfg.n_clusters) return NULL;
+  return owner(r, cluster, lc);
+}
+#define ROUTE_NODE(call)                                                         \
+  uint32_t lc;                                                                   \
+  shard_t* sh = node_owner(r, cluster, &lc);                                     \
+  if (!sh) return fail(-EINVAL, "cluster/node out of bounds");                   \
+  return call;
+
+int raft_ref_read_queue(raft_ref_t* r, uint32_t cluster, uint32_t id, uint32_t which,
+                        raft_msg_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_queue(sh, lc, id, which, out, cap))
+}
+int raft_ref_write_queue(raft_ref_t* r, uint32_t cluster, uint32_t id, uint32_t which,
+                         const raft_msg_t* in, uint32_t count) {
+  ROUTE_NODE(sh_write_queue(sh, lc, id, which, in, count))
+}
+int raft_ref_read_arena(raft_ref_t* r, uint32_t cluster, uint32_t id, raft_entry_t* out,
+                        uint32_t cap) {
+  ROUTE_NODE(sh_read_arena(sh, lc, id, out, cap))
+}
+int raft_ref_write_arena(raft_ref_t* r, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+                         uint32_t count) {
+  ROUTE_NODE(sh_write_arena(sh, lc, id, in, count))
+}
+int raft_ref_read_commit_stream(raft_ref_t* r, uint32_t cluster, uint32_t id, uint32_t* out,
+                                uint32_t cap) {
+  ROUTE_NODE(sh_read_commit_stream(sh, lc, id, out, cap))
+}
+int raft_ref_write_commit_stream(raft_ref_t* r, uint32_t cluster, uint32_t id, const uint32_t* in,
+                                 uint32_t count) {
+  ROUTE_NODE(sh_write_commit_stream(sh, lc, id, in, count))
+}
+int raft_ref_read_trace(raft_ref_t* r, uint32_t cluster, uint32_t id, uint32_t first,
+                        raft_trace_event_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_trace(sh, lc, id, first, out, cap))
+}
+int raft_ref_read_trace_entries(raft_ref_t* r, uint32_t cluster, uint32_t id, uint32_t first,
+                                raft_entry_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_trace_entries(sh, lc, id, first, out, cap))
+}
+
+int raft_ref_read_counters(raft_ref_t* r, raft_counters_t* out) {
+  if (!r || !out) return fail(-EINVAL, "null argument");
+  memset(out, 0, sizeof *out);
+  out->first_violation_tick = UINT64_MAX;
+  for (int d = 0; d < r->G; ++d) {
+    raft_counters_t c = {0};
+    sh_read_counters(r->sh[d], &c);
+    out->node_ticks += c.node_ticks;
+    for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] += c.c[i];
+    if (c.first_violation_tick < out->first_violation_tick)
+      out->first_violation_tick = c.first_violation_tick;
+    if (c.payload_max > out->payload_max) out->payload_max = c.payload_max;
+  }
+  return 0;
+}

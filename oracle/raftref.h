@@ -28,7 +28,11 @@ int raft_ref_abi_version(void);
 void raft_ref_default_config(raft_sim_config_t* cfg);
 int raft_ref_create(const raft_sim_config_t* cfg, raft_ref_t** out);
 int raft_ref_set_threads(raft_ref_t* sim, int threads);
+/* CPU baseline mode: visit only the ticks at which some node of a cluster can act (the same
+ * discrete-event skipping the tick kernel does per wave); results are identical. */
+int raft_ref_set_idle_skip(raft_ref_t* sim, int on);
 int raft_ref_step(raft_ref_t* sim, uint32_t n_ticks);
+int raft_ref_set_tick(raft_ref_t* sim, uint64_t tick);
 int raft_ref_step_async(raft_ref_t* sim, uint32_t n_ticks);   /* = raft_ref_step (CPU) */
 int raft_ref_sync(raft_ref_t* sim);                             /* no-op */
 uint64_t raft_ref_tick(const raft_ref_t* sim);

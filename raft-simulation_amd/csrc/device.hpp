@@ -21,18 +21,16 @@ namespace rs {
 constexpr uint32_t INF = 0xFFFFFFFFu;
 enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
-constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;  // per-wave LDS counter slot holding min tick
-#ifdef RS_WAVESTATS
-constexpr int LCTR_WORDS = 64;   // diagnostic build: + the wave's phase clock
-#else
+constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min violation tick
+constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
-#endif
+static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
 constexpr int PW_WORDS = 64;   // 32 x u64 client-gap powers at the start of the block's LDS
 
 struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
   uint32_t hb, el_base, el_span, drop_ppm, dup_ppm, dmin, dmax, part_ppm, part_epoch,
-      client_ppm, variant;
+      client_ppm, variant, client_period, client_burst, client_redirects;
   uint32_t *flags, *masks, *term, *commit, *len, *deadline, *qmeta, *req_arr, *res_arr,
       *req_tail, *res_tail, *abase, *afront, *led, *trace_lo, *trace_hi;
   int32_t *next, *match;  // [N][NN], row p-1 for peer id p
@@ -49,7 +47,7 @@ struct DevSim {
   uint32_t TC, TE;
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
-  unsigned long long* ctr;  // [RAFT_CTR_COUNT] + [1] first violation (min)
+  unsigned long long* ctr;  // [RAFT_CTR_COUNT] sums, [+0] first violation (min), [+1] payload (max)
   const uint32_t* perm;     // [C] wave slot -> cluster (RAFT_SCHED_ALIGNED), null = identity
   uint32_t* skey;           // [C] RAFT_SCHED_ALIGNED: cluster's next event - next launch's t0
   uint32_t* shist;          // [SCHED_BUCKETS] histogram of skey (null: schedule fixed)
@@ -81,10 +79,9 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
   for (int i = 1; i < 32; ++i) pw[i] = (pw[i - 1] * pw[i - 1]) >> 32;
 }
 
-// Tick of the next client-set after tick t (t = -1 for the first): t + 1 + G(w), where G is the
-// greedy power search of SIM_SPEC §4 P0 over pw[top..0] (higher powers are 0 and never fire).
-__device__ inline uint32_t client_next_tick(int64_t t, uint32_t w, const unsigned long long* pw,
-                                            int top) {
+// Geometric gap G(w) of SIM_SPEC §4 P0: the greedy power search over pw[top..0] (higher powers
+// are 0 and never fire).
+__device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
   const uint64_t u = (uint64_t)w + 1;
   uint64_t acc = 1ull << 32, g = 0;
   for (int i = top; i >= 0; --i) {
@@ -94,8 +91,23 @@ __device__ inline uint32_t client_next_tick(int64_t t, uint32_t w, const unsigne
       g += 1ull << i;
     }
   }
-  const uint64_t nx = (uint64_t)(t + 1) + g;
-  return nx < 0xFFFFFFFFull ? (uint32_t)nx : 0xFFFFFFFFu;
+  return g;
+}
+
+// The client schedule (SIM_SPEC §4 P0, D14): bursts of B on-ticks at the start of every period P
+// (P = 0: every tick is on). Injections are spaced by geometric gaps counted in on-ticks: the tick
+// of on-tick number j, saturating at 2^32 - 1 = never (j >= 2^32 is never, as tick(j) >= j).
+__device__ inline uint32_t on_tick(uint64_t j, uint32_t P, uint32_t B) {
+  if (j >= 0xFFFFFFFFull) return 0xFFFFFFFFu;
+  const uint32_t j32 = (uint32_t)j;
+  const uint64_t t = P ? (uint64_t)(j32 / B) * P + j32 % B : j32;
+  return t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
+}
+// The next injection after the one at tick t (an on-tick), drawing gap word w.
+__device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const unsigned long long* pw,
+                                            int top, uint32_t P, uint32_t B) {
+  const uint64_t j = P ? (uint64_t)(t / P) * B + t % P : t;
+  return on_tick(j + 1 + client_gap(w, pw, top), P, B);
 }
 
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
@@ -154,24 +166,21 @@ __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
 }
 
 __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
-#ifndef RS_DIAG_NOCTR
   if (v) atomicAdd(&lctr[i], v);
-#endif
 }
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own
 // queue `which` (SIM_SPEC §4 P2: after every queued message whose arrival <= the new one).
-// Returns true when the message became the queue's head (the caller's head-register copy).
-__device__ __forceinline__ bool qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
+__device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
                                         QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr) {
   if (fault) {
     lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
-    return false;
+    return;
   }
   const uint32_t Q = S.Q;
   if (q.c >= Q) {
     lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
-    return false;
+    return;
   }
   uint32_t* qb = qslots(S, gi, which);
   const size_t qs = qstride(S);
@@ -197,7 +206,6 @@ __device__ __forceinline__ bool qinsert(const DevSim& S, uint32_t gi, uint32_t f
   q.c += 1;
   if (pos == 0) q.arr = arr;
   lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-  return pos == 0;
 }
 
 }  // namespace rs

@@ -34,17 +34,12 @@ static int fail(int code, const char* fmt, const char* detail = "") {
                                       hipGetErrorString(e_));                      \
   } while (0)
 
-#ifndef RS_SCHED_RANGE
-#define RS_SCHED_RANGE 1
-#endif
-#ifndef RS_RESORT_EVERY
-#define RS_RESORT_EVERY 1
-#endif
 
-struct raft_sim {
+struct Shard {
   raft_sim_config_t cfg;
   uint32_t N, Q, L, A, C, NN, tpl;
-  uint64_t tick;
+  uint64_t tick;        // the shard's next tick
+  uint64_t ticks_run;   // ticks simulated by this handle (node_ticks counts these)
   hipStream_t stream;
   hipEvent_t ev_start, ev_stop;
   std::vector<hipEvent_t> kev;   // per tick-kernel launch of a step: start, stop
@@ -55,16 +50,13 @@ struct raft_sim {
   uint32_t pending_launches;
   uint32_t last_launches;
   unsigned long long* client_pw;
-  // RAFT_SCHED_ALIGNED: bucket offsets and the wave-slot -> cluster map of the next launch;
-  // keys_fresh: d.skey/d.shist hold a matching key set (from the previous tick launch). Only the
-  // first launch computes them from the state: after host writes the keys are merely stale,
-  // which changes the packing (speed), never the results.
+  // RAFT_SCHED_ALIGNED: the spare histogram (the schedule kernel zeroes it while reading d.shist;
+  // the two swap every launch) and the wave-slot -> cluster map of the next launch. keys_fresh:
+  // d.skey/d.shist hold a matching key set (from the previous tick launch). Only the first launch
+  // computes them from the state: after host writes the keys are merely stale, which changes the
+  // packing (speed), never the results.
   uint32_t *soff, *sperm;
   bool keys_fresh;
-  // the packing is rebuilt before every RS_RESORT_EVERY-th launch (and the first): steady-state
-  // clusters keep their phase relationship (equal heartbeat periods), so a packing stays aligned
-  // over several launches and the key/histogram/scan/scatter work is paid once per K launches
-  uint32_t nlaunch;
 };
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -76,7 +68,7 @@ void raft_sim_default_config(raft_sim_config_t* c) {
   memset(c, 0, sizeof *c);
   c->n_clusters = 1; c->nodes = 5; c->log_cap = 64; c->inbox_cap = 16; c->seed = 42;
   c->hb = 3000; c->el_base = 5000; c->el_span = 5000; c->dmin = 1; c->dmax = 1;
-  c->part_epoch = 1000;
+  c->part_epoch = 1000; c->n_devices = 1;
 }
 
 static int validate_cfg(const raft_sim_config_t* c) {
@@ -99,11 +91,19 @@ static int validate_cfg(const raft_sim_config_t* c) {
   if (c->schedule > RAFT_SCHED_FIXED) return fail(-EINVAL, "schedule: 0 (aligned) or 1 (fixed)");
   if (c->trace_cap > (1u << 20) || c->trace_entry_cap > (1u << 24))
     return fail(-EINVAL, "trace_cap <= 2^20, trace_entry_cap <= 2^24");
+  if ((uint64_t)c->cluster_offset + c->n_clusters > (1ull << 32))
+    return fail(-EINVAL, "cluster_offset + n_clusters must be <= 2^32");
+  if ((uint64_t)c->nodes * c->nodes * c->n_clusters >= (1ull << 31))
+    return fail(-EINVAL, "nodes^2 * n_clusters must be < 2^31");
+  if (c->client_period && (c->client_burst < 1 || c->client_burst > c->client_period))
+    return fail(-EINVAL, "client_burst must be 1..client_period");
+  if (c->client_redirects > 16) return fail(-EINVAL, "client_redirects <= 16");
+  if (c->n_devices < 0 || c->n_devices > 64) return fail(-EINVAL, "n_devices 0..64");
   return 0;
 }
 
 template <typename T>
-static int dalloc(raft_sim* s, T** p, size_t count) {
+static int dalloc(Shard* s, T** p, size_t count) {
   void* v = nullptr;
   hipError_t e = hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T));
   if (e != hipSuccess) return fail(-ENOMEM, "hipMalloc failed: %s", hipGetErrorString(e));
@@ -112,7 +112,7 @@ static int dalloc(raft_sim* s, T** p, size_t count) {
   return 0;
 }
 
-void raft_sim_destroy(raft_sim_t* s) {
+static void sh_destroy(Shard* s) {
   if (!s) return;
   (void)hipSetDevice(s->cfg.device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
@@ -124,14 +124,9 @@ void raft_sim_destroy(raft_sim_t* s) {
   delete s;
 }
 
-int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
-  if (!cfg || !out) return fail(-EINVAL, "null argument");
-  int rc = validate_cfg(cfg);
-  if (rc) return rc;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-    return fail(-EIO, "no HIP device visible: libraftsim.so requires an MI355X (gfx950)");
-  if (cfg->device < 0 || cfg->device >= ndev) return fail(-EINVAL, "device ordinal out of range");
+// One shard: cfg holds its own cluster count, global offset and device (validated by the caller).
+static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
+  int rc = 0;
   HIP_OK(hipSetDevice(cfg->device));
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, cfg->device));
@@ -139,7 +134,7 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
     return fail(-EIO, "device is %s; libraftsim.so is built for gfx950", prop.gcnArchName);
   HIP_OK(rs::configure_kernels());
 
-  raft_sim* s = new raft_sim();
+  Shard* s = new Shard();
   s->cfg = *cfg;
   s->N = cfg->nodes; s->Q = cfg->inbox_cap; s->L = cfg->log_cap; s->C = cfg->n_clusters;
   s->A = cfg->arena_cap ? cfg->arena_cap : 4 * cfg->log_cap;
@@ -153,6 +148,8 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
   d.drop_ppm = cfg->drop_ppm; d.dup_ppm = cfg->dup_ppm; d.dmin = cfg->dmin; d.dmax = cfg->dmax;
   d.part_ppm = cfg->part_ppm; d.part_epoch = cfg->part_epoch; d.client_ppm = cfg->client_ppm;
   d.variant = cfg->variant_flags;
+  d.client_period = cfg->client_period; d.client_burst = cfg->client_burst;
+  d.client_redirects = cfg->client_redirects;
   d.SC = cfg->commit_stream_cap;
   d.TC = cfg->trace_cap;
   d.TE = cfg->trace_entry_cap;
@@ -167,25 +164,25 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
                       &d.req_arr, &d.res_arr, &d.req_tail, &d.res_tail, &d.abase, &d.afront,
                       &d.led, &d.trace_lo, &d.trace_hi};
   for (uint32_t** p : hot)
-    if ((rc = dalloc(s, p, NN))) { raft_sim_destroy(s); return rc; }
+    if ((rc = dalloc(s, p, NN))) { sh_destroy(s); return rc; }
   if ((rc = dalloc(s, &d.next, NN * s->N)) || (rc = dalloc(s, &d.match, NN * s->N)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
       (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.cl, (size_t)s->C * 8)) ||
-      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 1)) || (rc = dalloc(s, &s->client_pw, 32)) ||
+      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 2)) || (rc = dalloc(s, &s->client_pw, 32)) ||
       (rc = dalloc(s, &d.ccount, NN)) ||
       (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1))) ||
       (rc = dalloc(s, &d.tr, NN * std::max<uint32_t>(d.TC, 1) * 32)) ||
       (rc = dalloc(s, &d.tcount, NN)) ||
       (rc = dalloc(s, &d.tent, NN * std::max<uint32_t>(d.TE, 1))) ||
       (rc = dalloc(s, &d.tecount, NN))) {
-    raft_sim_destroy(s);
+    sh_destroy(s);
     return rc;
   }
   d.client_pw = s->client_pw;
   if (cfg->schedule == RAFT_SCHED_ALIGNED) {
     if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
         (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) || (rc = dalloc(s, &s->sperm, s->C))) {
-      raft_sim_destroy(s);
+      sh_destroy(s);
       return rc;
     }
   }
@@ -206,20 +203,21 @@ int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
       (e = hipMemsetAsync(d.tecount, 0, NN * 4, s->stream)) != hipSuccess ||
       (d.shist && (e = hipMemsetAsync(d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream)) != hipSuccess) ||
       (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT + 1, 0, 8, s->stream)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
       (e = rs::launch_init(d, s->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
-    raft_sim_destroy(s);
+    sh_destroy(s);
     return fail(-EIO, "HIP error during create: %s", hipGetErrorString(e));
   }
   *out = s;
   return 0;
 }
 
-int raft_sim_step_async(raft_sim_t* s, uint32_t n_ticks) {
-  if (!s) return fail(-EINVAL, "null sim");
-  if (s->tick + n_ticks > 0xFFFFFFFFull) return fail(-EINVAL, "tick counter would exceed 2^32");
+// Enqueue n_ticks on the shard's stream. s->tick advances launch by launch, so after a failure it
+// still names the tick the state has reached (the handle is then poisoned anyway).
+static int sh_step_async(Shard* s, uint32_t n_ticks) {
   HIP_OK(hipSetDevice(s->cfg.device));
   uint32_t launches = s->pending_launches;
   if (!s->pending) {
@@ -229,49 +227,35 @@ int raft_sim_step_async(raft_sim_t* s, uint32_t n_ticks) {
   }
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
-    const uint32_t t0 = (uint32_t)s->tick + done;
-    bool keyless = false;
+    const uint32_t t0 = (uint32_t)s->tick;
     if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
       // pack clusters with the same next event onto the same waves for this launch: keys and
       // histogram come from the previous tick launch, or are recomputed from the state
-      if (!s->d.perm || s->nlaunch % RS_RESORT_EVERY == 0) {
-        if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
-#if RS_SCHED_RANGE
-        // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
-        std::swap(s->d.shist, s->soff);
-#endif
-        s->d.perm = s->sperm;
-        s->keys_fresh = true;
-      }
-      // only the launch before a rebuild writes keys and histogram for it
-      if ((s->nlaunch + 1) % RS_RESORT_EVERY != 0) {
-        keyless = true;
-        s->keys_fresh = false;
-      } else {
-        s->keys_fresh = true;
-      }
+      if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
+      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
+      // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
+      std::swap(s->d.shist, s->soff);
+      s->d.perm = s->sperm;
+      s->keys_fresh = true;
     }
-    rs::DevSim dl = s->d;
-    if (keyless) dl.shist = nullptr;
-    ++s->nlaunch;
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;
       HIP_OK(hipEventCreate(&e));
       s->kev.push_back(e);
     }
     HIP_OK(hipEventRecord(s->kev[2 * launches], s->stream));
-    HIP_OK(rs::launch_tick(dl, t0, nt, s->stream));
+    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
     HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
     done += nt;
+    s->tick += nt;
+    s->ticks_run += nt;
     ++launches;
     s->pending_launches = launches;
   }
-  s->tick += n_ticks;
   return 0;
 }
 
-int raft_sim_sync(raft_sim_t* s) {
+static int sh_sync(Shard* s) {
   if (!s) return fail(-EINVAL, "null sim");
   HIP_OK(hipSetDevice(s->cfg.device));
   if (!s->pending) {
@@ -296,47 +280,34 @@ int raft_sim_sync(raft_sim_t* s) {
   return 0;
 }
 
-int raft_sim_step(raft_sim_t* s, uint32_t n_ticks) {
-  const int rc = raft_sim_step_async(s, n_ticks);
-  return rc ? rc : raft_sim_sync(s);
-}
 
-int raft_sim_last_step_timing(raft_sim_t* s, double* avg_kernel_ms, uint32_t* launches) {
-  if (!s || !avg_kernel_ms || !launches) return fail(-EINVAL, "null argument");
-  *avg_kernel_ms = s->last_ms;
-  *launches = s->last_launches;
-  return 0;
-}
-
-uint64_t raft_sim_tick(const raft_sim_t* s) { return s ? s->tick : 0; }
-
-static int check_range(raft_sim* s, uint32_t c0, uint32_t nc) {
+static int check_range(Shard* s, uint32_t c0, uint32_t nc) {
   if (!s) return fail(-EINVAL, "null sim");
   if ((uint64_t)c0 + nc > s->C) return fail(-EINVAL, "cluster range out of bounds");
   return 0;
 }
 
 // Slot 0 of node gi's queue `which` in the slot-major queue buffer [2][Q][NN] (slot stride NN).
-static uint32_t* qring(raft_sim* s, uint32_t gi, uint32_t which) {
+static uint32_t* qring(Shard* s, uint32_t gi, uint32_t which) {
   return s->d.qbuf + ((size_t)which * s->Q * s->NN + gi) * 8;
 }
 
-static int check_node(raft_sim* s, uint32_t cluster, uint32_t id) {
+static int check_node(Shard* s, uint32_t cluster, uint32_t id) {
   if (!s) return fail(-EINVAL, "null sim");
   if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
   return 0;
 }
 
 template <typename T>
-static hipError_t d2h(raft_sim* s, T* host, const T* dev, size_t count) {
+static hipError_t d2h(Shard* s, T* host, const T* dev, size_t count) {
   return hipMemcpyAsync(host, dev, count * sizeof(T), hipMemcpyDeviceToHost, s->stream);
 }
 template <typename T>
-static hipError_t h2d(raft_sim* s, T* dev, const T* host, size_t count) {
+static hipError_t h2d(Shard* s, T* dev, const T* host, size_t count) {
   return hipMemcpyAsync(dev, host, count * sizeof(T), hipMemcpyHostToDevice, s->stream);
 }
 
-int raft_sim_read_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
+static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   if (!out) return fail(-EINVAL, "null output");
@@ -376,7 +347,7 @@ int raft_sim_read_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_node_t* ou
   return 0;
 }
 
-int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   if (!in) return fail(-EINVAL, "null input");
@@ -427,7 +398,7 @@ int raft_sim_write_nodes(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_nod
   return 0;
 }
 
-int raft_sim_read_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+static int sh_read_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which,
                         raft_msg_t* out, uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -447,7 +418,7 @@ int raft_sim_read_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t w
   return (int)cnt;
 }
 
-int raft_sim_write_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t which,
+static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which,
                          const raft_msg_t* in, uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -481,7 +452,7 @@ int raft_sim_write_queue(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t 
   return 0;
 }
 
-int raft_sim_read_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
+static int sh_read_arena(Shard* s, uint32_t cluster, uint32_t id, raft_entry_t* out,
                         uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -496,7 +467,7 @@ int raft_sim_read_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, raft_entry
   return (int)s->A;
 }
 
-int raft_sim_write_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+static int sh_write_arena(Shard* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
                          uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -512,7 +483,7 @@ int raft_sim_write_arena(raft_sim_t* s, uint32_t cluster, uint32_t id, const raf
   return 0;
 }
 
-int raft_sim_read_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t* out,
+static int sh_read_commit_stream(Shard* s, uint32_t cluster, uint32_t id, uint32_t* out,
                                 uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -529,7 +500,7 @@ int raft_sim_read_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, ui
   return (int)kept;
 }
 
-int raft_sim_write_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, const uint32_t* in,
+static int sh_write_commit_stream(Shard* s, uint32_t cluster, uint32_t id, const uint32_t* in,
                                  uint32_t count) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -554,7 +525,7 @@ int raft_sim_write_commit_stream(raft_sim_t* s, uint32_t cluster, uint32_t id, c
 // F3 rings: copy the retained items with index >= first (oldest first), at most cap of them;
 // `strict` rejects a `first` that has been overwritten instead of starting at the oldest kept.
 template <typename T>
-static int read_ring(raft_sim* s, const uint32_t* dcount, const T* dring, uint32_t R, uint32_t gi,
+static int read_ring(Shard* s, const uint32_t* dcount, const T* dring, uint32_t R, uint32_t gi,
                      uint32_t first, T* out, uint32_t cap, bool strict) {
   uint32_t cnt = 0;
   HIP_OK(d2h(s, &cnt, dcount + gi, 1));
@@ -574,7 +545,7 @@ static int read_ring(raft_sim* s, const uint32_t* dcount, const T* dring, uint32
   return (int)n;
 }
 
-int raft_sim_read_trace(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+static int sh_read_trace(Shard* s, uint32_t cluster, uint32_t id, uint32_t first,
                         raft_trace_event_t* out, uint32_t cap) {
   static_assert(sizeof(raft_trace_event_t) == 128, "trace record is 32 words");
   int rc = check_node(s, cluster, id);
@@ -585,7 +556,7 @@ int raft_sim_read_trace(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t f
                    s->d.TC, cluster * s->N + id - 1, first, out, cap, false);
 }
 
-int raft_sim_read_trace_entries(raft_sim_t* s, uint32_t cluster, uint32_t id, uint32_t first,
+static int sh_read_trace_entries(Shard* s, uint32_t cluster, uint32_t id, uint32_t first,
                                 raft_entry_t* out, uint32_t cap) {
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
@@ -595,7 +566,7 @@ int raft_sim_read_trace_entries(raft_sim_t* s, uint32_t cluster, uint32_t id, ui
                    cluster * s->N + id - 1, first, out, cap, true);
 }
 
-int raft_sim_read_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
+static int sh_read_clusters(Shard* s, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
@@ -606,7 +577,7 @@ int raft_sim_read_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, raft_cluster
   return 0;
 }
 
-int raft_sim_write_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
+static int sh_write_clusters(Shard* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
@@ -618,19 +589,20 @@ int raft_sim_write_clusters(raft_sim_t* s, uint32_t c0, uint32_t nc, const raft_
   return 0;
 }
 
-int raft_sim_read_counters(raft_sim_t* s, raft_counters_t* out) {
+static int sh_read_counters(Shard* s, raft_counters_t* out) {
   if (!s || !out) return fail(-EINVAL, "null argument");
   HIP_OK(hipSetDevice(s->cfg.device));
-  unsigned long long buf[RAFT_CTR_COUNT + 1];
+  unsigned long long buf[RAFT_CTR_COUNT + 2];
   HIP_OK(hipMemcpyAsync(buf, s->d.ctr, sizeof buf, hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] = buf[i];
   out->first_violation_tick = buf[RAFT_CTR_COUNT];
-  out->node_ticks = (uint64_t)s->NN * s->tick;
+  out->payload_max = buf[RAFT_CTR_COUNT + 1];
+  out->node_ticks = (uint64_t)s->NN * s->ticks_run;
   return 0;
 }
 
-int raft_sim_digest(raft_sim_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
+static int sh_digest(Shard* s, uint32_t c0, uint32_t nc, uint64_t* out) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
   if (!out) return fail(-EINVAL, "null output");
@@ -646,3 +618,237 @@ int raft_sim_digest(raft_sim_t* s, uint32_t c0, uint32_t nc, uint64_t* out) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The handle: n_devices shards, each a contiguous cluster range [C*d/G, C*(d+1)/G) on device
+// (device + d) mod the visible devices, with its own stream. The global cluster id keys Philox
+// (SIM_SPEC D13), so every G gives bit-identical clusters; calls addressed to clusters are routed
+// to their shard and counters are reduced on the host (SUM; MIN first violation; MAX payload).
+// Across processes (torchrun, one rank per GPU) bench.py reduces the same vector over RCCL.
+struct raft_sim {
+  raft_sim_config_t cfg;
+  std::vector<Shard*> sh;
+  std::vector<uint32_t> lo;   // shard d owns clusters [lo[d], lo[d+1])
+  uint64_t tick;
+  bool poisoned;              // a step failed part-way: the state no longer matches `tick`
+};
+
+void raft_sim_destroy(raft_sim_t* r) {
+  if (!r) return;
+  for (Shard* s : r->sh) sh_destroy(s);
+  delete r;
+}
+
+int raft_sim_create(const raft_sim_config_t* cfg, raft_sim_t** out) {
+  if (!cfg || !out) return fail(-EINVAL, "null argument");
+  int rc = validate_cfg(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(-EIO, "no HIP device visible: libraftsim.so requires an MI355X (gfx950)");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(-EINVAL, "device ordinal out of range");
+  const uint32_t G = std::min<uint32_t>(cfg->n_devices > 1 ? cfg->n_devices : 1, cfg->n_clusters);
+  for (uint32_t d = 0; d < G; ++d) {
+    const int dev = (cfg->device + (int)d) % ndev;
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return fail(-EIO, "device is %s; libraftsim.so is built for gfx950", prop.gcnArchName);
+    HIP_OK(hipSetDevice(dev));
+    HIP_OK(rs::configure_kernels());
+  }
+  raft_sim* r = new raft_sim();
+  r->cfg = *cfg;
+  for (uint32_t d = 0; d <= G; ++d) r->lo.push_back((uint32_t)((uint64_t)cfg->n_clusters * d / G));
+  for (uint32_t d = 0; d < G; ++d) {
+    raft_sim_config_t c = *cfg;
+    c.n_clusters = r->lo[d + 1] - r->lo[d];
+    c.cluster_offset = cfg->cluster_offset + r->lo[d];
+    c.device = (cfg->device + (int)d) % ndev;
+    c.n_devices = 1;
+    Shard* s = nullptr;
+    if ((rc = sh_create(&c, &s))) {
+      raft_sim_destroy(r);
+      return rc;
+    }
+    r->sh.push_back(s);
+  }
+  *out = r;
+  return 0;
+}
+
+// SIM_SPEC D1: no deadline or arrival may reach 2^32 - 1, the "never" marker.
+static bool horizon_ok(const raft_sim_config_t& c, uint64_t tick, uint32_t n) {
+  const uint64_t longest = std::max<uint64_t>({c.hb, (uint64_t)c.el_base + c.el_span, c.dmax});
+  return tick + n + longest < 0xFFFFFFFFull;
+}
+
+int raft_sim_step_async(raft_sim_t* r, uint32_t n_ticks) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if (r->poisoned) return fail(-EIO, "a previous step failed part-way; the handle is unusable");
+  if (!horizon_ok(r->cfg, r->tick, n_ticks))
+    return fail(-ERANGE, "tick + n_ticks + the longest timer would reach 2^32-1");
+  for (Shard* s : r->sh) {
+    const int rc = sh_step_async(s, n_ticks);
+    if (rc) {
+      r->poisoned = true;
+      return rc;
+    }
+  }
+  r->tick += n_ticks;
+  return 0;
+}
+
+int raft_sim_sync(raft_sim_t* r) {
+  if (!r) return fail(-EINVAL, "null sim");
+  for (Shard* s : r->sh) {
+    const int rc = sh_sync(s);
+    if (rc) {
+      r->poisoned = true;
+      return rc;
+    }
+  }
+  return 0;
+}
+
+int raft_sim_step(raft_sim_t* r, uint32_t n_ticks) {
+  const int rc = raft_sim_step_async(r, n_ticks);
+  return rc ? rc : raft_sim_sync(r);
+}
+
+uint64_t raft_sim_tick(const raft_sim_t* r) { return r ? r->tick : 0; }
+
+int raft_sim_set_tick(raft_sim_t* r, uint64_t tick) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if (!horizon_ok(r->cfg, tick, 0)) return fail(-ERANGE, "tick beyond the 32-bit horizon");
+  for (Shard* s : r->sh) {
+    const int rc = sh_sync(s);
+    if (rc) return rc;
+    s->tick = tick;
+    s->keys_fresh = false;      // the packing keys are relative to the next launch's first tick
+  }
+  r->tick = tick;
+  return 0;
+}
+
+int raft_sim_last_step_timing(raft_sim_t* r, double* avg_kernel_ms, uint32_t* launches) {
+  if (!r || !avg_kernel_ms || !launches) return fail(-EINVAL, "null argument");
+  double sum = 0;
+  uint32_t n = 0;
+  for (Shard* s : r->sh) {
+    sum += s->last_ms * s->last_launches;
+    n += s->last_launches;
+  }
+  *avg_kernel_ms = n ? sum / n : 0.0;
+  *launches = r->sh.empty() ? 0 : r->sh[0]->last_launches;
+  return 0;
+}
+
+// The shard owning cluster c, and c's index inside it.
+static Shard* owner(raft_sim* r, uint32_t c, uint32_t* lc) {
+  const size_t d = std::upper_bound(r->lo.begin() + 1, r->lo.end() - 1, c) - (r->lo.begin() + 1);
+  *lc = c - r->lo[d];
+  return r->sh[d];
+}
+
+// Run `fn(shard, local c0, count, offset into the caller's range)` over the per-shard pieces.
+template <typename F>
+static int pieces(raft_sim* r, uint32_t c0, uint32_t nc, F fn) {
+  if (!r) return fail(-EINVAL, "null sim");
+  if ((uint64_t)c0 + nc > r->cfg.n_clusters) return fail(-EINVAL, "cluster range out of bounds");
+  for (uint32_t done = 0; done < nc;) {
+    uint32_t lc;
+    Shard* s = owner(r, c0 + done, &lc);
+    const uint32_t n = std::min(s->C - lc, nc - done);
+    const int rc = fn(s, lc, n, (size_t)done);
+    if (rc) return rc;
+    done += n;
+  }
+  return 0;
+}
+
+int raft_sim_read_nodes(raft_sim_t* r, uint32_t c0, uint32_t nc, raft_node_t* out) {
+  if (!out) return fail(-EINVAL, "null output");
+  return pieces(r, c0, nc, [&](Shard* s, uint32_t lc, uint32_t n, size_t off) {
+    return sh_read_nodes(s, lc, n, out + off * r->cfg.nodes);
+  });
+}
+int raft_sim_write_nodes(raft_sim_t* r, uint32_t c0, uint32_t nc, const raft_node_t* in) {
+  if (!in) return fail(-EINVAL, "null input");
+  return pieces(r, c0, nc, [&](Shard* s, uint32_t lc, uint32_t n, size_t off) {
+    return sh_write_nodes(s, lc, n, in + off * r->cfg.nodes);
+  });
+}
+int raft_sim_read_clusters(raft_sim_t* r, uint32_t c0, uint32_t nc, raft_cluster_t* out) {
+  if (!out) return fail(-EINVAL, "null output");
+  return pieces(r, c0, nc, [&](Shard* s, uint32_t lc, uint32_t n, size_t off) {
+    return sh_read_clusters(s, lc, n, out + off);
+  });
+}
+int raft_sim_write_clusters(raft_sim_t* r, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
+  if (!in) return fail(-EINVAL, "null input");
+  return pieces(r, c0, nc, [&](Shard* s, uint32_t lc, uint32_t n, size_t off) {
+    return sh_write_clusters(s, lc, n, in + off);
+  });
+}
+int raft_sim_digest(raft_sim_t* r, uint32_t c0, uint32_t nc, uint64_t* out) {
+  if (!out) return fail(-EINVAL, "null output");
+  return pieces(r, c0, nc, [&](Shard* s, uint32_t lc, uint32_t n, size_t off) {
+    return sh_digest(s, lc, n, out + off);
+  });
+}
+
+#define ROUTE_NODE(call)                                                                  \
+  if (!r || cluster >= r->cfg.n_clusters) return fail(-EINVAL, "cluster/node out of bounds"); \
+  uint32_t lc;                                                                            \
+  Shard* s = owner(r, cluster, &lc);                                                      \
+  return call;
+
+int raft_sim_read_queue(raft_sim_t* r, uint32_t cluster, uint32_t id, uint32_t which,
+                        raft_msg_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_queue(s, lc, id, which, out, cap))
+}
+int raft_sim_write_queue(raft_sim_t* r, uint32_t cluster, uint32_t id, uint32_t which,
+                         const raft_msg_t* in, uint32_t count) {
+  ROUTE_NODE(sh_write_queue(s, lc, id, which, in, count))
+}
+int raft_sim_read_arena(raft_sim_t* r, uint32_t cluster, uint32_t id, raft_entry_t* out,
+                        uint32_t cap) {
+  ROUTE_NODE(sh_read_arena(s, lc, id, out, cap))
+}
+int raft_sim_write_arena(raft_sim_t* r, uint32_t cluster, uint32_t id, const raft_entry_t* in,
+                         uint32_t count) {
+  ROUTE_NODE(sh_write_arena(s, lc, id, in, count))
+}
+int raft_sim_read_commit_stream(raft_sim_t* r, uint32_t cluster, uint32_t id, uint32_t* out,
+                                uint32_t cap) {
+  ROUTE_NODE(sh_read_commit_stream(s, lc, id, out, cap))
+}
+int raft_sim_write_commit_stream(raft_sim_t* r, uint32_t cluster, uint32_t id, const uint32_t* in,
+                                 uint32_t count) {
+  ROUTE_NODE(sh_write_commit_stream(s, lc, id, in, count))
+}
+int raft_sim_read_trace(raft_sim_t* r, uint32_t cluster, uint32_t id, uint32_t first,
+                        raft_trace_event_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_trace(s, lc, id, first, out, cap))
+}
+int raft_sim_read_trace_entries(raft_sim_t* r, uint32_t cluster, uint32_t id, uint32_t first,
+                                raft_entry_t* out, uint32_t cap) {
+  ROUTE_NODE(sh_read_trace_entries(s, lc, id, first, out, cap))
+}
+
+int raft_sim_read_counters(raft_sim_t* r, raft_counters_t* out) {
+  if (!r || !out) return fail(-EINVAL, "null argument");
+  memset(out, 0, sizeof *out);
+  out->first_violation_tick = UINT64_MAX;
+  for (Shard* s : r->sh) {
+    raft_counters_t c;
+    const int rc = sh_read_counters(s, &c);
+    if (rc) return rc;
+    out->node_ticks += c.node_ticks;
+    for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] += c.c[i];
+    out->first_violation_tick = std::min(out->first_violation_tick, c.first_violation_tick);
+    out->payload_max = std::max(out->payload_max, c.payload_max);
+  }
+  return 0;
+}

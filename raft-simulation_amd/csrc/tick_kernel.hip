@@ -8,12 +8,6 @@
 // VALU instructions and one ballot.
 #include "device.hpp"
 
-// waves per workgroup of the tick kernel: a workgroup's LDS and slot are released only when its
-// last wave ends, so smaller workgroups refill the CU sooner when wave lifetimes differ
-#ifndef RS_WPB
-#define RS_WPB 1
-#endif
-
 namespace rs {
 
 __device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) {
@@ -78,40 +72,6 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   }
   cl[CELLW - 1] = pack;
   sentmask |= 1u << p;
-}
-
-// Head-register cache of one queue (RS_HEADREG): while the queue is non-empty, m0.y..w and m1
-// of its head message. `dirty`: the head exists only here (it landed in an empty queue and
-// nothing has been queued behind it yet) and is written to its ring slot only when a second
-// message arrives or the launch ends; a steady-state message that is popped on the next tick
-// never reaches memory.
-struct HeadR {
-  uint4 m0, m1;
-  bool dirty;
-};
-
-template <bool HR>
-__device__ __forceinline__ bool qpush(const DevSim& S, uint32_t gi, uint32_t fault, int which,
-                                      QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr, HeadR& h) {
-  if constexpr (!HR) {
-    return qinsert(S, gi, fault, which, q, m0, m1, lctr);
-  } else {
-    if (!fault && q.c == 0) {       // as qinsert into an empty queue, without the store
-      h.m0 = m0; h.m1 = m1; h.dirty = true;
-      q.c = 1; q.arr = m0.x; q.tail = m0.x;
-      lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-      return true;
-    }
-    if (h.dirty && !fault) {
-      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, which) + q.h * qstride(S));
-      hp[0] = make_uint4(q.arr, h.m0.y, h.m0.z, h.m0.w);
-      hp[1] = h.m1;
-      h.dirty = false;
-    }
-    const bool nh = qinsert(S, gi, fault, which, q, m0, m1, lctr);
-    if (nh) { h.m0 = m0; h.m1 = m1; }
-    return nh;
-  }
 }
 
 // A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are
@@ -200,7 +160,8 @@ __device__ __forceinline__ void spec_handle(
     uint32_t id, int k, int bl, uint32_t sgi, uint32_t peers, uint4 m0, uint4 m1,
     uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
     uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
-    uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg) {
+    uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg,
+    bool& rearm) {
   const uint32_t A = S.A;
   if (which < 0) {
     if (n.role == RAFT_LEADER) {                                  // heartbeat
@@ -246,7 +207,10 @@ __device__ __forceinline__ void spec_handle(
                       (mt == lt && ma >= n.len);
       const uint32_t grant = mterm == n.term && (n.vf == 0 || n.vf == src) && up;
       ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
-      if (grant) n.vf = src;
+      if (grant) {
+        n.vf = src;
+        rearm = true;                       // Figure 2: granting a vote resets the timer
+      }
       emit = 3;
       break;
     }
@@ -255,6 +219,7 @@ __device__ __forceinline__ void spec_handle(
       emit = 3;
       if (mterm < n.term) break;
       n.role = RAFT_FOLLOWER; n.votes = 0; n.lid = src;
+      rearm = true;                         // AppendEntries from the current leader
       if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
       if (!consistent) break;
       // first conflict in [b, min(len, b + pcnt)); the payload is read from the sender's arena,
@@ -295,7 +260,10 @@ __device__ __forceinline__ void spec_handle(
       break;
     }
     case RAFT_MSG_CLIENT_SET: {                                   // as client-set-handler 151-160
-      if (n.role != RAFT_LEADER) break;
+      if (n.role != RAFT_LEADER) {
+        emit = 4;                                                 // redirect-client
+        break;
+      }
       pkind = PLAN_ENTRY; ppoff = n.term; ppcnt = ma;
       pold_base = n.base;
       if (n.base + n.len != n.front) {
@@ -375,69 +343,36 @@ constexpr int wave_lds_words() {
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + RS_WPB * wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
+  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
 }
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
-// faithful kernel carries none of its code.
-#ifndef RS_QRESET
-#define RS_QRESET 1
-#endif
-#ifndef RS_SCHED_RANGE
-#define RS_SCHED_RANGE 1
-#endif
-#ifndef RS_SCHED_FUSED
-#define RS_SCHED_FUSED 0
-#endif
-#ifndef RS_HEADREG
-#define RS_HEADREG 0
-#endif
+// faithful kernel carries none of its code. One wave per workgroup: wave lifetimes differ by up
+// to 2x under load, and a multi-wave workgroup holds its CU slot and LDS until its slowest wave
+// ends (measured: 4-wave workgroups 1-2 % slower on C2/C3/C4).
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
 #endif
-#ifdef RS_WAVESTATS
-// Wave-level phase clock in LDS (wst: 11 accumulators + the last stamp): every active lane
-// writes the same values, so a stamp inside a divergent region still charges the wave.
-#define RS_STAMP(i)                                        \
-  do {                                                     \
-    __builtin_amdgcn_s_waitcnt(0);                         \
-    const uint64_t now_ = clock64();                       \
-    const uint64_t last_ = wst[11];                        \
-    wst[i] += now_ - last_;                                \
-    wst[11] = now_;                                        \
-    __builtin_amdgcn_s_waitcnt(0);                         \
-  } while (0)
-#else
-#define RS_STAMP(i) do { } while (0)
-#endif
 
 template <int N, bool TRACE, bool SPEC>
-__global__ void __launch_bounds__(64 * RS_WPB) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
-  constexpr int WAVE_WORDS = wave_lds_words<N, SPEC>();
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // block-shared: the client-gap power table (SIM_SPEC P0), then one region per wave
+  const int lane = threadIdx.x;
+  // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters and leader rows
   unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
-  if (threadIdx.x < 32) pw[threadIdx.x] = S.client_pw[threadIdx.x];
-  __syncthreads();
-  uint32_t* cells = smem + PW_WORDS + wv * WAVE_WORDS;
+  if (lane < 32) pw[lane] = S.client_pw[lane];
+  uint32_t* cells = smem + PW_WORDS;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+  __builtin_amdgcn_wave_barrier();
 
-#ifndef RS_SPREAD
-#define RS_SPREAD 1
-#endif
-  // With RAFT_SCHED_ALIGNED, neighbouring wave slots hold clusters with the same next event, so
-  // they are active on the same ticks. A multi-wave workgroup's waves therefore take slots
-  // 1/RS_WPB of the grid apart, so waves sharing a CU are active on different ticks (with the
-  // default one-wave workgroups this is the identity).
-  const uint32_t wave = (RS_SPREAD && S.perm) ? wv * gridDim.x + blockIdx.x : blockIdx.x * RS_WPB + wv;
+  const uint32_t wave = blockIdx.x;
   const int cs = lane / N, k0 = lane - cs * N;
   const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
   const bool active = lane < CPW * N && slot < S.C;
@@ -448,12 +383,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   const uint32_t NN = S.NN, A = S.A;
 
   NodeR n = {};
-  // Head registers (RS_HEADREG bit 0 REQ, bit 1 RES): while a queue is non-empty, its head
-  // message is also held here (words y..w of m0, all of m1; m0.x is the queue's `arr`). The queue
-  // in HBM stays complete (write-through), so a pop needs no load on its critical path; the new
-  // head is loaded at the pop and is not waited on until the next pop.
-  constexpr bool HRQ = (RS_HEADREG & 1) != 0, HRS = (RS_HEADREG & 2) != 0;
-  HeadR hq = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), false}, hs = hq;
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
   uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
   if (active) {
@@ -467,14 +396,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     n.rq.tail = S.req_tail[gi]; n.rs.tail = S.res_tail[gi];
     n.base = S.abase[gi]; n.front = S.afront[gi]; n.led = S.led[gi];
     n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
-    if (HRQ && n.rq.c) {
-      const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 0) + n.rq.h * qstride(S));
-      hq.m0 = hp[0]; hq.m1 = hp[1];
-    }
-    if (HRS && n.rs.c) {
-      const uint4* hp = reinterpret_cast<const uint4*>(qslots(S, gi, 1) + n.rs.h * qstride(S));
-      hs.m0 = hp[0]; hs.m1 = hp[1];
-    }
     hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
     cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
     if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
@@ -493,16 +414,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
-#ifdef RS_WAVETIME
-  const uint64_t wt0 = wall_clock64();
-  uint32_t wt_active = 0;
-#endif
-#ifdef RS_WAVESTATS
-  uint32_t wstat_active = 0;
-  uint64_t* wst = reinterpret_cast<uint64_t*>(lctr + 32);
-  if (lane < 12) wst[lane] = lane == 11 ? clock64() : 0ull;
-  __builtin_amdgcn_wave_barrier();
-#endif
 
   const uint32_t tend = t0 + nt;
   for (uint32_t t = t0;; ++t) {
@@ -511,10 +422,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // the wave jumps over them: discrete-event skipping with tick-exact results.
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
-    RS_STAMP(0);
-#ifdef RS_WAVETIME
-    ++wt_active;
-#endif
     const bool live = active && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
     // address and shuffle index the active-tick phases use out of the tick loop, where each would
@@ -534,7 +441,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       __builtin_amdgcn_wave_barrier();
     }
 
-    // ---------------------------------------------------------------- P0 client injection (D9)
+    // ---------------------------------------------------------- P0 client injection (D9, D14)
     bool inj = false;
     uint32_t injv = 0;
     const bool cinj = active && t == cnext;
@@ -547,7 +454,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           injv = d.z;
         }
         ccount += 1;
-        cnext = client_next_tick(t, d.w, pw, S.client_top);
+        cnext = client_next_tick(t, d.w, pw, S.client_top, S.client_period, S.client_burst);
       }
     }
 
@@ -558,12 +465,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (__ballot(inj)) {
       if (inj) {
         if (live && n.rq.c == 0) dcs = true;
-        else qpush<HRQ>(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                        make_uint4(0, 0, 0, 0), lctr, hq);
+        else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                     make_uint4(0, 0, 0, 0), lctr);
       }
     }
 
-    RS_STAMP(1);
     // ---------------------------------------------------------------- P1 one event per node
     const bool req_ok = live && (dcs || n.rq.arr <= t);
     const bool res_ok = live && n.rs.arr <= t;
@@ -575,6 +481,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, preloc = 0,
              papplied = 0;
     bool elected = false, mchg = false;
+    uint32_t pmax = 0;                                        // largest AE payload emitted
     uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
     if (live && (req_ok || res_ok || t >= n.deadline)) {
       // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
@@ -597,8 +504,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
           lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
         } else {
-          qpush<HRQ>(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                     make_uint4(0, 0, 0, 0), lctr, hq);
+          qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
+                  make_uint4(0, 0, 0, 0), lctr);
         }
       }
       if (which >= 0 && !(dcs && which == 0)) {
@@ -609,43 +516,15 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const QueueR q = which ? n.rs : n.rq;
         const uint32_t* qb = qslots(S, sgi, which);
         const size_t qs = qstride(S);
-        const bool hreg = which ? HRS : HRQ;
-        if (hreg) {
-          const uint4 h0 = which ? hs.m0 : hq.m0;
-          m0 = make_uint4(q.arr, h0.y, h0.z, h0.w);
-          m1 = which ? hs.m1 : hq.m1;
-          if (which) hs.dirty = false;       // consumed: a register-only head never reaches memory
-          else hq.dirty = false;
-        } else {
-          const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
-          m0 = sp[0];
-          m1 = sp[1];
-        }
+        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
+        m0 = sp[0];
+        m1 = sp[1];
         const uint32_t nh = wrapq(q.h + 1, S.Q);
-#if RS_QRESET
         // Only a queue that stays non-empty has a next head. Its arrival is known without a load
         // when one message remains or all queued ones share the head's arrival (the queue is
         // sorted, so head == tail means all equal): then nothing this tick waits on memory.
         uint32_t narr = INF;
-        if (q.c > 1) {
-          if (q.c == 2 || q.arr == q.tail) narr = q.tail;
-          else narr = qb[nh * qs];
-          if (hreg) {
-            const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
-            const uint4 n0 = np[0], n1 = np[1];
-            if (which) { hs.m0 = n0; hs.m1 = n1; }
-            else { hq.m0 = n0; hq.m1 = n1; }
-          }
-        }
-#else
-        const uint32_t narr = qb[nh * qs];
-        if (hreg) {
-          const uint4* np = reinterpret_cast<const uint4*>(qb + nh * qs);
-          const uint4 n0 = np[0], n1 = np[1];
-          if (which) { hs.m0 = n0; hs.m1 = n1; }
-          else { hq.m0 = n0; hq.m1 = n1; }
-        }
-#endif
+        if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
         if (!have_w && n.role != RAFT_LEADER) {
           w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
           have_w = true;
@@ -655,16 +534,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         r.c -= 1;
         r.arr = r.c ? narr : INF;
         r.tail = r.c ? r.tail : 0u;
-#if RS_QRESET
         // A queue that drains restarts its ring at slot 0 (the ring position is not state: reads
         // linearise from the head). Steady-state traffic then lands in slots 0..P-1, where a
         // cluster's nodes are adjacent, instead of walking all Q slots of the [slot][node] layout.
         if (!r.c) r.h = 0;
-#endif
         if (which) n.rs = r;
         else n.rq = r;
       }
-      RS_STAMP(2);
       const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
                      mpoff = m1.w;
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
@@ -681,15 +557,18 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       // Every throw site of the reference precedes every mutation of its handler (SIM_SPEC D8),
       // so each case decides `fault` first and only then updates the node in place.
       uint32_t fault = 0, ev = 0;
-      int emit = 0;                 // 1 request-vote bcast, 2 append-entries bcast, 3 one reply
+      // 1 request-vote bcast, 2 append-entries bcast, 3 one reply, 4 redirect-client
+      int emit = 0;
       int nm = 0;                   // next/match: 1 init, 2 clear, 3 dec next[src], 4 set src
       uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);  // reply cell words
       uint32_t appended = 0, applied = 0;
+      const bool was_leader = n.role == RAFT_LEADER;
+      bool rearm = false;           // SPEC: the event resets the election timer (SIM_SPEC §8)
 
       if constexpr (SPEC) {
         spec_handle<N, MAJ>(S, n, lsw, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
                             emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
-                            pold_base, preloc, papplied, elected, mchg);
+                            pold_base, preloc, papplied, elected, mchg, rearm);
       } else if (which < 0) {
         if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
           ev = 7;
@@ -782,7 +661,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             break;
           }
           case RAFT_MSG_CLIENT_SET: {                        // client-set-handler 151-160
-            if (n.role != RAFT_LEADER) break;                // redirect-client only
+            if (n.role != RAFT_LEADER) {                     // redirect-client: no state change
+              emit = 4;
+              break;
+            }
             if (n.len + 1 > S.L) {
               fault = RAFT_FAULT_OVERFLOW;
               break;
@@ -857,15 +739,17 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         elected = false;
         mchg = false;
       } else {
+        // generate-timeout (core.clj:171-174) for the next wait: every event re-arms the timer
+        // (D4); Spec-Raft keeps Raft's timers (SIM_SPEC §8)
         if (n.role == RAFT_LEADER) {
-          n.deadline = t + S.hb;
-        } else {
+          if (!SPEC || ev == 7 || elected) n.deadline = t + S.hb;
+        } else if (!SPEC || ev == 6 || rearm || was_leader) {
           if (!have_w) w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+          have_w = true;
           n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
         }
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
         // leader-state words (cold, in HBM)
-        RS_STAMP(3);
         if (nm == 1 || nm == 2) {
           const int32_t first_next = (int32_t)((SPEC ? n.len : n.commit) + 1);
 #pragma unroll
@@ -891,7 +775,34 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           lctr_add(lctr, RAFT_CTR_LEADERS, 1);
           n.led = n.term;
         }
-        RS_STAMP(4);
+        // ------------------------------------------------ redirect-client (server.clj:62-63)
+        // to the :leader-id, else (rand-nth cluster) by w2 of the EVENT draw (core.clj:153-155);
+        // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
+        // {a, b + 1} arriving at t + 1 outside the fault model. A redirect to the node itself
+        // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
+        if (emit == 4) {
+          emit = 0;
+          if (mb >= S.client_redirects) {
+            lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
+          } else {
+            uint32_t dst = n.lid;
+            if (!dst) {
+              if (!have_w) w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+              const uint32_t i = __umulhi(w.z, N - 1);
+              dst = i + 1 < id ? i + 1 : i + 2;
+            }
+            lctr_add(lctr, RAFT_CTR_REDIRECTS, 1);
+            *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
+                make_uint2(dst == id ? mb + 1 : 0u, ma);
+            if (dst != id) {
+              uint32_t* cl =
+                  mycells + (k * (N - 1) + (dst - 1 < (uint32_t)k ? dst - 1 : dst - 2)) * CELLW;
+              cell_put(cl, make_uint4(RAFT_MSG_CLIENT_SET, 0, 0, mb + 1), make_uint4(0, 0, 0, 0));
+              cl[CELLW - 1] = 1u | 1u << 16;
+            }
+            sentmask |= 1u << dst;
+          }
+        }
         // ------------------------------------------------ emission (rpc / respond)
         if (emit) {
           bool part = false;
@@ -915,7 +826,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             int32_t nxs[N];
 #pragma unroll
             for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? lsw.next(p) : 0;
-            RS_STAMP(9);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -928,6 +838,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                   ep = 1; et = e.x; evl = e.y;
                 }
                 const uint32_t pc = n.len - prev;
+                pmax = pc > pmax ? pc : pmax;
                 ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
                                 n.commit, prev);
                 rb = make_uint4(et, evl, pc ? n.base + prev : 0, 0);
@@ -942,13 +853,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                   pc = n.len - start - 1;
                   po = pc ? n.base + start + 1 : 0;
                 }
+                pmax = pc > pmax ? pc : pmax;
                 ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
                                 n.commit, (uint32_t)prev);
                 rb = make_uint4(et, evl, po, 0);
               }
               cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
             }
-            RS_STAMP(10);
+            if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -961,7 +873,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
-    RS_STAMP(5);
     // ---------------------------------------------------------------- P2 network delivery
     if (__ballot(sentmask != 0)) {
       // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
@@ -976,21 +887,22 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       uint32_t copy = 0;
       while (inmask) {
         const int s = __builtin_ctz(inmask);
-        const uint2* cl =
-            reinterpret_cast<const uint2*>(mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
-        const uint2 c0 = cl[0], c1 = cl[1], c2 = cl[2];
         const uint2 sr = *reinterpret_cast<const uint2*>(mysrec + s * SRECW);
+        uint2 c0 = make_uint2(RAFT_MSG_CLIENT_SET, sr.x), c1 = make_uint2(0, 0),
+              c2 = make_uint2(0, 1u | 1u << 16);           // a redirect to this node itself
+        if (s != k) {
+          const uint2* cl = reinterpret_cast<const uint2*>(
+              mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
+          c0 = cl[0]; c1 = cl[1]; c2 = cl[2];
+        }
         const uint32_t d = copy == 0 ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
         const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
-        const uint4 q0 = make_uint4(t + d, c0.x, sr.x, sr.y), q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
-        if (which) {
-          qpush<HRS>(S, sgi, n.fault, 1, q, q0, q1, lctr, hs);
-          n.rs = q;
-        } else {
-          qpush<HRQ>(S, sgi, n.fault, 0, q, q0, q1, lctr, hq);
-          n.rq = q;
-        }
+        const uint4 q0 = make_uint4(t + d, c0.x, s != k ? sr.x : 0u, sr.y),
+                    q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
+        qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
+        if (which) n.rs = q;
+        else n.rq = q;
         if (++copy >= (c2.y >> 16)) {
           copy = 0;
           inmask &= inmask - 1;
@@ -998,7 +910,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
-    RS_STAMP(6);
     // ---------------------------------------------------------------- P3 log writes
     // m entries were added at position n.len - m (appended_at, -1 when none)
     const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
@@ -1049,7 +960,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
-    RS_STAMP(7);
     // ---------------------------------------------------------------- P4 invariant checker
     // the majority-match scan can raise hwm only when the leader's log reaches past it
     const bool mcheck = (elected || mchg) && n.len > hidx;
@@ -1131,33 +1041,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
       }
     }
-    RS_STAMP(8);
     wnext = next_event();
-#ifdef RS_WAVESTATS
-    ++wstat_active;
-    RS_STAMP(0);
-#endif
   }
-#ifdef RS_WAVESTATS   // diagnostic build only: per-wave active ticks into two counters unused by C2
-  if (lane == 0) {
-    atomicAdd(&S.ctr[RAFT_CTR_PAYLOAD_EVICTED], (unsigned long long)wstat_active);
-    atomicMax(&S.ctr[RAFT_CTR_HALT_OVERFLOW], (unsigned long long)wstat_active);
-    const int wslot[11] = {RAFT_CTR_DROPPED, RAFT_CTR_PARTITIONED, RAFT_CTR_DUPLICATED,
-                          RAFT_CTR_OVERFLOW, RAFT_CTR_TO_HALTED, RAFT_CTR_CLIENT_INJECTED,
-                          RAFT_CTR_ENTRIES_APPLIED, RAFT_CTR_VIOL_ELECTION, RAFT_CTR_VIOL_LOG,
-                          RAFT_CTR_EV_CS, RAFT_CTR_ENTRIES_APPENDED};
-    for (int i = 0; i < 11; ++i) atomicAdd(&S.ctr[wslot[i]], (unsigned long long)wst[i]);
-    if (wstat_active > 40) atomicAdd(&S.ctr[RAFT_CTR_HALT_NPE], 1ull);
-    if (wstat_active > 60) atomicAdd(&S.ctr[RAFT_CTR_HALT_CCE], 1ull);
-    if (wstat_active > 80) atomicAdd(&S.ctr[RAFT_CTR_HALT_IOOBE], 1ull);
-    if (wstat_active > 100) atomicAdd(&S.ctr[RAFT_CTR_VIOL_COMPLETE], 1ull);
-  }
-#endif
 
   // ---------------------------------------------------------------- write back
   if (S.shist) {
     // RAFT_SCHED_ALIGNED: the cluster's next event relative to the next launch, counted into the
-    // bucket histogram the host turns into the next launch's wave packing (sched_scan/scatter)
+    // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
     const uint32_t me = active && !n.fault ? min(n.deadline, min(n.rq.arr, n.rs.arr)) : INF;
     uint32_t cm = active ? cnext : INF;
 #pragma unroll
@@ -1174,14 +1064,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     S.masks[gi] = n.votes | n.keys << 16;
     S.term[gi] = n.term; S.commit[gi] = n.commit; S.len[gi] = n.len; S.deadline[gi] = n.deadline;
     S.qmeta[gi] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
-    if (HRQ && hq.dirty) {
-      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, 0) + n.rq.h * qstride(S));
-      hp[0] = make_uint4(n.rq.arr, hq.m0.y, hq.m0.z, hq.m0.w); hp[1] = hq.m1;
-    }
-    if (HRS && hs.dirty) {
-      uint4* hp = reinterpret_cast<uint4*>(qslots(S, gi, 1) + n.rs.h * qstride(S));
-      hp[0] = make_uint4(n.rs.arr, hs.m0.y, hs.m0.z, hs.m0.w); hp[1] = hs.m1;
-    }
     S.req_arr[gi] = n.rq.arr; S.res_arr[gi] = n.rs.arr;
     S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
     S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
@@ -1199,34 +1081,16 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-#ifdef RS_DIAG_NOFLUSH
-  if (false) {
-#else
   if (lane < RAFT_CTR_COUNT) {
-#endif
     const uint32_t v = lctr[lane];
     if (v) atomicAdd(&S.ctr[lane], (unsigned long long)v);
   } else if (lane == LCTR_FIRSTVIOL) {
     const uint32_t v = lctr[lane];
     if (v != INF) atomicMin(&S.ctr[RAFT_CTR_COUNT], (unsigned long long)v);
+  } else if (lane == LCTR_PAYLOADMAX) {
+    const uint32_t v = lctr[lane];
+    if (v) atomicMax(&S.ctr[RAFT_CTR_COUNT + 1], (unsigned long long)v);
   }
-#ifdef RS_WAVETIME   // diagnostic build: wave lifetime (100 MHz ticks) into counters C2 never uses
-  if (lane == 0 && t0 > 0) {
-    const unsigned long long dur = wall_clock64() - wt0;
-    const bool slow = dur >= 15000;
-    atomicAdd(&S.ctr[RAFT_CTR_DROPPED], dur);
-    atomicAdd(&S.ctr[RAFT_CTR_PARTITIONED], (unsigned long long)wt_active);
-    if (slow) {
-      atomicAdd(&S.ctr[RAFT_CTR_DUPLICATED], 1ull);
-      atomicAdd(&S.ctr[RAFT_CTR_OVERFLOW], (unsigned long long)wt_active);
-      atomicAdd(&S.ctr[RAFT_CTR_CLIENT_INJECTED], dur);
-      if (wave >= 4096) atomicAdd(&S.ctr[RAFT_CTR_ENTRIES_APPLIED], 1ull);
-    }
-    atomicMax(&S.ctr[RAFT_CTR_TO_HALTED],
-              (unsigned long long)dur << 40 | (unsigned long long)(wt_active & 0xFFFF) << 24 | wave);
-    if (wt_active > 40) atomicAdd(&S.ctr[RAFT_CTR_VIOL_ELECTION], 1ull);
-  }
-#endif
 }
 
 // RAFT_SCHED_ALIGNED wave packing: a counting sort of the clusters by their next event tick
@@ -1234,7 +1098,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 // launch's first tick. Clusters with the same next event then share waves, and a steady-state
 // cluster's later events (heartbeat every hb ticks) stay aligned with its wave mates', so a
 // wave's active ticks are nearly those of one cluster instead of the union of twelve. The order
-// inside a bucket is whatever the scatter's atomics give: any packing yields identical results.
+// inside a bucket is whatever the LDS atomics give: any packing yields identical results.
 //
 // sched_key_kernel: keys + histogram from the state (first launch, or after host writes);
 // the tick kernel writes both at its end for the next launch.
@@ -1253,87 +1117,11 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   atomicAdd(&S.shist[key], 1u);
 }
 
-// One block: exclusive scan of the histogram into off[], which the scatter consumes; the
-// histogram is cleared for the tick kernel to refill.
-__global__ void __launch_bounds__(1024) sched_scan_kernel(uint32_t* hist, uint32_t* off) {
-  constexpr uint32_t PER = SCHED_BUCKETS / 1024;
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x;
-  uint32_t v[PER], sum = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < PER; ++i) {
-    v[i] = hist[t * PER + i];
-    hist[t * PER + i] = 0;
-    sum += v[i];
-  }
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {        // Hillis-Steele inclusive scan
-    const uint32_t x = t >= d ? part[t - d] : 0u;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - sum;
-#pragma unroll
-  for (uint32_t i = 0; i < PER; ++i) {
-    off[t * PER + i] = run;
-    run += v[i];
-  }
-}
-
-__global__ void sched_scatter_kernel(DevSim S, uint32_t* off, uint32_t* perm) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= S.C) return;
-  perm[atomicAdd(&off[S.skey[c]], 1u)] = c;
-}
-
-hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
-  hipLaunchKernelGGL(sched_key_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, t0);
-  return hipGetLastError();
-}
-
-// scan + scatter in one workgroup: the bucket offsets live in LDS (16,384 x 4 B = 64 KiB), so
-// the scatter's position claims are LDS atomics on one CU instead of device-scope atomics that
-// cross XCDs, and the schedule costs one launch instead of two. Thread t owns buckets
-// [16t, 16t + 16); the block-wide exclusive scan of the per-thread sums is a wave scan
-// (__shfl_up) plus the 16 wave totals, parked in off[0..15] before the offsets are written.
-__global__ void __launch_bounds__(1024) sched_perm_kernel(DevSim S, uint32_t* perm) {
-  constexpr uint32_t PER = SCHED_BUCKETS / 1024;
-  __shared__ uint32_t off[SCHED_BUCKETS];
-  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t v[PER], sum = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < PER; ++i) {
-    v[i] = S.shist[t * PER + i];
-    S.shist[t * PER + i] = 0;
-    sum += v[i];
-  }
-  uint32_t inc = sum;                                 // inclusive scan inside the wave
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t x = __shfl_up(inc, d);
-    if (lane >= d) inc += x;
-  }
-  if (lane == 63) off[w] = inc;
-  __syncthreads();
-  uint32_t run = inc - sum;
-  for (uint32_t j = 0; j < w; ++j) run += off[j];
-  __syncthreads();
-#pragma unroll
-  for (uint32_t i = 0; i < PER; ++i) {
-    off[t * PER + i] = run;
-    run += v[i];
-  }
-  __syncthreads();
-  for (uint32_t c = t; c < S.C; c += 1024) perm[atomicAdd(&off[S.skey[c]], 1u)] = c;
-}
-
 // Scan + scatter without global atomics: block b of SCHED_RANGE_BLOCKS owns the key range
 // [b*KB, (b+1)*KB). It sums the histogram below its range (its base), scans its own KB buckets
 // into LDS offsets, then reads every cluster's key and places the clusters of its range with LDS
-// atomics. Each block reads all keys (L2-resident, 4 B per cluster), and there is one launch
-// instead of two. The histogram is double-buffered: this kernel reads S.shist and zeroes `zero`,
+// atomics. Each block reads all keys (L2-resident, 4 B per cluster); 13 us per launch at C2 (a
+// separate scan and a device-atomic scatter took 22.5 us). The histogram is double-buffered: this kernel reads S.shist and zeroes `zero`,
 // which the next tick launch fills (the host swaps the two).
 constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
 __global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* zero,
@@ -1402,18 +1190,14 @@ __global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* z
   }
 }
 
-hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st) {
-#if RS_SCHED_RANGE
-  hipLaunchKernelGGL(sched_range_kernel, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, off,
+hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
+  hipLaunchKernelGGL(sched_key_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, t0);
+  return hipGetLastError();
+}
+
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, hipStream_t st) {
+  hipLaunchKernelGGL(sched_range_kernel, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, zero,
                      perm);
-#elif RS_SCHED_FUSED
-  (void)off;
-  hipLaunchKernelGGL(sched_perm_kernel, dim3(1), dim3(1024), 0, st, S, perm);
-#else
-  hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(1024), 0, st, S.shist, off);
-  hipLaunchKernelGGL(sched_scatter_kernel, dim3((S.C + 255) / 256), dim3(256), 0, st, S, off,
-                     perm);
-#endif
   return hipGetLastError();
 }
 
@@ -1432,7 +1216,8 @@ __global__ void init_kernel(DevSim S) {
     uint32_t first = INF;
     if (S.client_ppm) {
       const uint4 d = philox(S.goff + c, P_CLIENT << 8, 0, 1, S.key0, S.key1);
-      first = client_next_tick(-1, d.x, S.client_pw, S.client_top);
+      first = on_tick(client_gap(d.x, S.client_pw, S.client_top), S.client_period,
+                      S.client_burst);
     }
     for (int i = 0; i < 8; ++i) S.cl[c * 8 + i] = 0;
     S.cl[c * 8 + 3] = first;
@@ -1508,11 +1293,10 @@ void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
   constexpr int CPW = 64 / N;
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = (S.C + CPW - 1) / CPW;
-  const uint32_t blocks = (waves + RS_WPB - 1) / RS_WPB;
   if (S.TC)
-    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(blocks), dim3(64 * RS_WPB), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(waves), dim3(64), lds, st, S, t0, nt);
   else
-    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(blocks), dim3(64 * RS_WPB), lds, st, S, t0, nt);
+    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(waves), dim3(64), lds, st, S, t0, nt);
 }
 
 template <int N>

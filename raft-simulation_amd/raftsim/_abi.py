@@ -14,7 +14,7 @@ COUNTER_NAMES = ["ev_rv", "ev_ae", "ev_cs", "ev_vr", "ev_ar", "ev_timeout", "ev_
                  "leaders", "sent", "delivered", "dropped", "partitioned", "duplicated",
                  "overflow", "to_halted", "client_injected", "halt_ioobe", "halt_npe", "halt_cce",
                  "halt_overflow", "entries_appended", "entries_applied", "payload_evicted",
-                 "viol_election", "viol_log", "viol_complete"]
+                 "viol_election", "viol_log", "viol_complete", "redirects", "client_abandoned"]
 
 
 class Config(C.Structure):
@@ -27,7 +27,9 @@ class Config(C.Structure):
                 ("client_ppm", C.c_uint32), ("variant_flags", C.c_uint32),
                 ("device", C.c_int32), ("ticks_per_launch", C.c_uint32),
                 ("commit_stream_cap", C.c_uint32), ("trace_cap", C.c_uint32),
-                ("trace_entry_cap", C.c_uint32), ("schedule", C.c_uint32)]
+                ("trace_entry_cap", C.c_uint32), ("schedule", C.c_uint32),
+                ("client_period", C.c_uint32), ("client_burst", C.c_uint32),
+                ("client_redirects", C.c_uint32), ("n_devices", C.c_int32)]
 
 
 class Node(C.Structure):
@@ -89,11 +91,12 @@ class Cluster(C.Structure):
 
 class Counters(C.Structure):
     _fields_ = [("node_ticks", C.c_uint64), ("first_violation_tick", C.c_uint64),
-                ("c", C.c_uint64 * len(COUNTER_NAMES))]
+                ("c", C.c_uint64 * len(COUNTER_NAMES)), ("payload_max", C.c_uint64)]
 
     def as_dict(self):
         d = {name: self.c[i] for i, name in enumerate(COUNTER_NAMES)}
         d["node_ticks"] = self.node_ticks
+        d["payload_max"] = self.payload_max
         d["first_violation_tick"] = (None if self.first_violation_tick == 2 ** 64 - 1
                                      else self.first_violation_tick)
         return d
@@ -108,6 +111,7 @@ _SIGS = {
     "step_async": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sync": (C.c_int, [C.c_void_p]),
     "tick": (C.c_uint64, [C.c_void_p]),
+    "set_tick": (C.c_int, [C.c_void_p, C.c_uint64]),
     "read_nodes": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Node)]),
     "write_nodes": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(Node)]),
     "read_queue": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(Msg),

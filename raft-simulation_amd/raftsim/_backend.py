@@ -32,7 +32,7 @@ class Backend:
     def __init__(self, lib_path, prefix, **config):
         self._lib = C.CDLL(str(lib_path))
         self._fns = _abi.bind(self._lib, prefix, optional=("last_step_timing",))
-        if self._fns["abi_version"]() != 1:
+        if self._fns["abi_version"]() != 2:
             raise RaftSimError("ABI version mismatch")
         self.config = make_config(self._fns, **config)
         h = C.c_void_p()
@@ -78,6 +78,11 @@ class Backend:
     @property
     def tick(self):
         return int(self._fns["tick"](self._h))
+
+    def set_tick(self, tick):
+        """Resume at `tick` (state restored through the write_* calls; SIM_SPEC deadlines are
+        absolute ticks)."""
+        self._check(self._fns["set_tick"](self._h, int(tick)))
 
     def last_step_timing(self):
         ms, n = C.c_double(), C.c_uint32()

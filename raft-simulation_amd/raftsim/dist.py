@@ -3,7 +3,7 @@
 Clusters are independent and Philox streams are keyed by the global cluster id (SIM_SPEC D13),
 so a rank simulates a contiguous range of clusters with no data-path exchange. The only
 collective is the end-of-run reduction of the counter vector (SUM) and the first-violation tick
-(MIN): a few hundred bytes, latency-bound, over RCCL (torch.distributed backend "nccl") on the GPU
+(MIN) and the largest append-entries payload (MAX): a few hundred bytes, latency-bound, over RCCL (torch.distributed backend "nccl") on the GPU
 box or gloo in the CPU tests.
 """
 from __future__ import annotations
@@ -23,15 +23,21 @@ def reduce_counters(c: dict, device=None) -> dict:
     import torch
     import torch.distributed as dist
 
-    names = sorted(k for k in c if k != "first_violation_tick")
+    names = sorted(k for k in c if k not in ("first_violation_tick", "payload_max"))
     v = torch.tensor([int(c[k]) for k in names], dtype=torch.int64, device=device)
     dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    pm = None
+    if "payload_max" in c:
+        pm = torch.tensor([int(c["payload_max"])], dtype=torch.int64, device=device)
+        dist.all_reduce(pm, op=dist.ReduceOp.MAX)
     fv = c.get("first_violation_tick")
     f = torch.tensor([NONE_TICK if fv is None else int(fv)], dtype=torch.int64, device=device)
     dist.all_reduce(f, op=dist.ReduceOp.MIN)
     out = dict(zip(names, (int(x) for x in v.tolist())))
     fmin = int(f.item())
     out["first_violation_tick"] = None if fmin == NONE_TICK else fmin
+    if pm is not None:
+        out["payload_max"] = int(pm.item())
     return out
 
 

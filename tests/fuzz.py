@@ -31,6 +31,9 @@ def random_config(rng):
         cfg.update(part_ppm=500000, part_epoch=rng.randint(1, 4))
     if rng.random() < 0.3:
         cfg["client_ppm"] = rng.choice([100000, 500000])
+    cfg["client_redirects"] = rng.choice([0, 0, 1, 3])
+    if rng.random() < 0.2:
+        cfg.update(client_period=rng.randint(2, 9), client_burst=1)
     return cfg
 
 
@@ -76,7 +79,7 @@ def _random_msg(rng, typ, arrival, dst, N, nodes):
     src = rng.choice([p for p in range(1, N + 1) if p != dst])
     term = rng.randint(1, 5)
     if typ == "client-set":
-        return msg(typ, arrival, command=rng.randint(0, 2))
+        return msg(typ, arrival, command=rng.randint(0, 2), hops=rng.randint(0, 3))
     if typ == "request-vote":
         return msg(typ, arrival, term=term, candidate_id=src, last_log_index=rng.randint(0, 4),
                    last_log_term=None if rng.random() < 0.3 else _entry(rng))

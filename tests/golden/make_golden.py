@@ -26,10 +26,24 @@ CASES = {
                                  client_ppm=5000, log_cap=64), gid=1, ticks=20000, trace=False),
     "variant_n3": dict(cfg=dict(nodes=3, seed=17, variant_flags=1, client_ppm=150,
                                 drop_ppm=50000, log_cap=64), gid=2, ticks=30000, trace=False),
+    # BASELINE config 4 shape: 7 nodes, 4096-entry logs, bursty client traffic that follows
+    # redirect-client to the leader (SIM_SPEC D14/D15): multi-thousand-entry AppendEntries batches
+    "c4_bursts_n7": dict(cfg=dict(nodes=7, seed=3, log_cap=4096, client_ppm=500000,
+                                  client_period=8192, client_burst=2048, client_redirects=4),
+                         gid=5, ticks=36000, trace=False),
+    # config 3 faults with bursts and redirects on 5 nodes, full event trace
+    "c3_bursts_n5": dict(cfg=dict(nodes=5, seed=1, drop_ppm=100000, dup_ppm=10000, dmin=1,
+                                  dmax=50, part_ppm=100000, log_cap=256, client_ppm=80000,
+                                  client_period=16384, client_burst=2048, client_redirects=4),
+                         gid=9, ticks=40000, trace=True),
     # F4 Spec-Raft control (SIM_SPEC §8) with faults and client traffic, full event trace
     "spec_n5": dict(cfg=dict(nodes=5, seed=19, variant_flags=2, client_ppm=2000, drop_ppm=100000,
                              dup_ppm=20000, dmin=1, dmax=30, part_ppm=100000, log_cap=256,
                              hb=300, el_base=500, el_span=500), gid=4, ticks=30000, trace=True),
+    "spec_bursts_n5": dict(cfg=dict(nodes=5, seed=23, variant_flags=2, drop_ppm=100000,
+                                    dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000, log_cap=1024,
+                                    client_ppm=200000, client_period=8192, client_burst=1024,
+                                    client_redirects=4), gid=6, ticks=40000, trace=True),
 }
 
 
@@ -62,7 +76,7 @@ def make(name, spec):
         nodes.append(n)
     out = {"config": spec["cfg"], "cluster_offset": spec["gid"], "ticks": spec["ticks"],
            "nodes": nodes, "hwm": list(c.hwm), "client": [c.client_next, c.client_count],
-           "counters": c.cnt,
+           "counters": c.cnt, "payload_max": c.payload_max,
            "first_violation_tick": c.first_violation}
     if spec["trace"]:
         out["events"] = c.hash_events

@@ -56,6 +56,8 @@ def check(name, make):
     for k, v in fx["counters"].items():
         assert c[k] == v, (name, k, c[k], v)
     assert c["first_violation_tick"] == fx["first_violation_tick"]
+    if "payload_max" in fx:
+        assert c["payload_max"] == fx["payload_max"], (name, c["payload_max"], fx["payload_max"])
     for i, text in fx.get("stdout", {}).items():
         assert be.edn_trace(0, int(i)) == text, (name, "stdout of node", i)
 

@@ -8,7 +8,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 ORACLE_LIB = ROOT / "oracle" / "build" / "libraftref.so"
 
-from raftsim._backend import Backend  # noqa: E402
+from raftsim._backend import Backend, RaftSimError  # noqa: E402,F401
 import pyref  # noqa: E402
 
 
@@ -90,6 +90,10 @@ def gpu(**cfg):
 
 def oracle_threads(be, n):
     be._lib.raft_ref_set_threads(be._h, n)
+
+
+def oracle_idle_skip(be, on=True):
+    be._lib.raft_ref_set_idle_skip(be._h, int(on))
 
 
 def cpu_threads():

@@ -389,6 +389,51 @@ def kat_client_set(view_of):
     assert v.node(2)["deadline"] >= 5000          # the event still re-arms the timer
 
 
+def kat_client_abandoned_without_redirects(view_of):
+    """client_redirects = 0: a redirect ends the command (counted as abandoned, nothing re-sent)."""
+    nodes = {1: node("leader", term=4, leader_id=1, ls={2: (1, 0)}), 2: node(term=4, leader_id=1)}
+    q = {(2, 0): [msg("client-set", 0, command=5)]}
+    v = view_of(Scenario(2, nodes, q))
+    v.step(3)
+    c = v.counters()
+    assert c["client_abandoned"] == 1 and c["redirects"] == 0 and v.log(1) == []
+
+
+def kat_redirect_to_leader(view_of):
+    """redirect-client (server.clj:62-63) to the :leader-id (core.clj:155), followed by the client:
+    the command reaches the leader one tick later and is appended (core.clj:156-160); a node with
+    a nil :leader-id redirects to (rand-nth cluster) (core.clj:154), drawn from w2 of its EVENT
+    draw (SIM_SPEC D15)."""
+    nodes = {1: node("leader", term=4, leader_id=1, ls={2: (1, 0), 3: (1, 0)}),
+             2: node("follwer", term=4, leader_id=1), 3: node(term=4)}
+    q = {(2, 0): [msg("client-set", 0, command=5)], (3, 0): [msg("client-set", 0, command=6)]}
+    v = view_of(Scenario(3, nodes, q, client_redirects=2))
+    w = pyref.philox((0, 3 | pyref.EVENT << 8, 0, 0), (42, 0))
+    target = [1, 2][(w[2] * 2) >> 32]
+    v.step(1)                                     # t0: both redirect (no state change)
+    assert v.log(1) == [] and v.node(2)["log_len"] == 0
+    assert v.node(2)["deadline"] >= 5000          # D4: the redirect still re-arms the timer
+    v.step(1)                                     # t1: the leader appends node 2's redirect
+    assert v.log(1) == [(4, 5)]
+    v.step(2 if target == 1 else 3)
+    assert v.log(1) == [(4, 5), (4, 6)]
+    c = v.counters()
+    assert c["redirects"] == (2 if target == 1 else 3) and c["client_abandoned"] == 0
+    assert c["ev_cs"] == (4 if target == 1 else 5) and c["sent"] == 0
+
+
+def kat_redirect_to_self(view_of):
+    """A stepped-down leader keeps its own :leader-id (candidate->follower, core.clj:75-78,130), so
+    redirect-client points the client back at it; each hop is an event until the hops run out."""
+    nodes = {1: node("follwer", term=5, leader_id=1, ls={2: (1, 0)}), 2: node(term=5)}
+    q = {(1, 0): [msg("client-set", 0, command=9)]}
+    v = view_of(Scenario(2, nodes, q, client_redirects=2))
+    v.step(4)
+    c = v.counters()
+    assert (c["ev_cs"], c["redirects"], c["client_abandoned"]) == (3, 2, 1)
+    assert v.log(1) == [] and v.node(1)["req_count"] == 0
+
+
 CHAN = "#<ManyToManyChannel clojure.core.async.impl.channels.ManyToManyChannel@%x>"
 
 
@@ -574,10 +619,35 @@ def kat_spec_vote_rules(view_of):
         assert r["fault"] == 0
 
 
-SPEC_ALL = [kat_spec_first_election, kat_spec_replication, kat_spec_truncate_on_conflict,
+def kat_spec_timers(view_of):
+    """Raft §5.2 timers (SIM_SPEC §8): a leader heartbeats every hb ticks whatever it handles; a
+    follower's election timer moves only for AppendEntries from the current leader, a granted
+    vote or its own timeout -- not for client-sets, redirects or stale messages."""
+    nodes = {1: node("leader", term=3, voted_for=1, leader_id=1, ls={2: (1, 0), 3: (1, 0)},
+                     deadline=10, last_led=3),
+             2: node("follower", term=3, leader_id=1, deadline=500),
+             3: node("follower", term=3, leader_id=1, deadline=BIG)}
+    q = {(1, 0): [msg("client-set", 0, command=7)],
+         (2, 0): [msg("client-set", 0, command=8),
+                  msg("request-vote", 1, term=2, candidate_id=3, last_log_index=0,
+                      last_log_term=None)]}
+    v = view_of(Scenario(3, nodes, q, variant_flags=SPEC, client_redirects=1))
+    v.step(1)                                    # t0: leader appends, follower 2 redirects
+    assert v.node(1)["deadline"] == 10 and v.node(2)["deadline"] == 500
+    v.step(2)                                    # t1: stale RV refused; t2: redirected set
+    assert v.node(2)["deadline"] == 500 and v.log(1) == [(3, 7), (3, 8)]
+    assert v.node(1)["deadline"] == 10
+    v.step(8)                                    # t10: heartbeat -> next one at 3010
+    assert v.node(1)["deadline"] == 3010
+    v.step(1)                                    # t11: AppendEntries re-arms the followers
+    assert v.node(2)["deadline"] >= 11 + 5000 and v.node(3)["deadline"] >= 11 + 5000
+
+
+SPEC_ALL = [kat_spec_timers, kat_spec_first_election, kat_spec_replication, kat_spec_truncate_on_conflict,
             kat_spec_commit_rule, kat_spec_vote_rules]
 
 ALL = [kat_majority, kat_first_election, kat_duplication, kat_truncate_crash, kat_cce, kat_npe,
        kat_partial_leader_state, kat_stale_step_down, kat_two_leaders_one_term, kat_vote_rules,
-       kat_variant_no_log_check, kat_client_set, kat_printed_trace, kat_printed_entries,
+       kat_variant_no_log_check, kat_client_set, kat_client_abandoned_without_redirects,
+       kat_redirect_to_leader, kat_redirect_to_self, kat_printed_trace, kat_printed_entries,
        *SPEC_ALL]

@@ -12,6 +12,11 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 FAULTS = dict(drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
+# SIM_SPEC D14/D15: bursts of client traffic with quiet gaps longer than the election timeout,
+# and clients that follow redirect-client (server.clj:62-63) to the leader
+BURSTS = dict(client_period=16384, client_burst=2048, client_redirects=4)
+C4_BURSTS = dict(log_cap=4096, client_ppm=500000, client_period=8192, client_burst=2048,
+                 client_redirects=4)
 
 CASES = {
     # C2 shape (no faults, no client traffic), smaller cluster count
@@ -59,6 +64,19 @@ CASES = {
     "spec_tight": dict(n_clusters=512, nodes=3, seed=49, client_ppm=30000, log_cap=24,
                        arena_cap=48, hb=40, el_base=60, el_span=60, variant_flags=2,
                        inbox_cap=3, **FAULTS),
+    # BASELINE config 4: 7 and 9 nodes, 4096-entry logs, bursts that build 1000+-entry batches
+    "c4_n7_bursts": dict(n_clusters=512, nodes=7, seed=3, commit_stream_cap=256, **C4_BURSTS),
+    "c4_n9_bursts": dict(n_clusters=256, nodes=9, seed=5, dup_ppm=20000, dmax=8, **C4_BURSTS),
+    # config 3 / 5 shapes with the bursty, redirect-following client
+    "c3_bursts": dict(n_clusters=2048, nodes=5, seed=1, client_ppm=80000, log_cap=256,
+                      **BURSTS, **FAULTS),
+    "spec_bursts": dict(n_clusters=1024, nodes=5, seed=61, client_ppm=80000, log_cap=1024,
+                        variant_flags=2, commit_stream_cap=64, **BURSTS, **FAULTS),
+    "spec_nolog_bursts": dict(n_clusters=1024, nodes=5, seed=63, client_ppm=80000, log_cap=1024,
+                              variant_flags=3, **BURSTS, **FAULTS),
+    "redirect_storm": dict(n_clusters=512, nodes=6, seed=65, client_ppm=1000000,
+                           client_period=300, client_burst=40, client_redirects=16, inbox_cap=4,
+                           log_cap=128, hb=50, el_base=80, el_span=80, **FAULTS),
 }
 
 
@@ -93,11 +111,44 @@ def test_gpu_matches_oracle(name):
     assert cg["node_ticks"] == cfg["n_clusters"] * cfg["nodes"] * 20000
 
 
-def test_gpu_c2_full_size():
-    """BASELINE config 2: 65,536 five-node clusters x 10k ticks, no faults, digest-equal."""
-    cfg = dict(n_clusters=65536, nodes=5, seed=42)
+@pytest.mark.parametrize("seed", [1, 42, 0xDEADBEEF, 0x1_2345_6789])
+def test_gpu_c2_full_size(seed):
+    """BASELINE config 2: 65,536 five-node clusters x 10k ticks, no faults, digest-equal, for the
+    seeds of SURVEY §8(d) and one above 2^32 (Philox key word 1 nonzero)."""
+    cfg = dict(n_clusters=65536, nodes=5, seed=seed)
     g, r = run_pair(cfg, 10000, 10000)
     assert g.counters() == r.counters()
+
+
+@pytest.mark.parametrize("nodes", [7, 9])
+def test_gpu_c4_logs_reach_capacity(nodes):
+    """BASELINE config 4 to its end: 4096-entry logs fill up under the bursty client, append-entries
+    carry 1000+ entries (core.clj:56-67 ships the whole suffix), and OVERFLOW halts appear (D8);
+    GPU == oracle on every cluster, counter and the payload maximum."""
+    cfg = dict(n_clusters=64, nodes=nodes, seed=7 + nodes, **C4_BURSTS)
+    g, r = run_pair(cfg, 110000, 55000)
+    cg, cr = g.counters(), r.counters()
+    assert cg == cr
+    assert cg["payload_max"] >= 1000 and cg["halt_overflow"] > 0
+    assert max(n["log_len"] for n in g.read_nodes()) >= 3000
+
+
+def test_gpu_sharded_handle_equals_single():
+    """n_devices = 3 (three shards; on a one-GPU box they share the device) reproduces the
+    one-shard handle: digests, counters, reads that cross shard boundaries, and resume."""
+    cfg = dict(n_clusters=1000, nodes=5, seed=71, client_ppm=80000, log_cap=256, **BURSTS,
+               **FAULTS)
+    one, three = helpers.gpu(**cfg), helpers.gpu(n_devices=3, **cfg)
+    for s in (one, three):
+        s.step(20000)
+    assert np.array_equal(one.digest(), three.digest())
+    assert one.counters() == three.counters()
+    assert one.read_nodes(300, 100) == three.read_nodes(300, 100)
+    assert one.read_clusters(330, 10) == three.read_clusters(330, 10)
+    for c in (332, 333, 334, 666, 667):
+        for i in (1, 5):
+            assert one.read_queue(c, i, 0) == three.read_queue(c, i, 0)
+            assert one.log(c, i) == three.log(c, i)
 
 
 def test_gpu_printed_trace_matches_oracle():
@@ -151,6 +202,8 @@ def test_gpu_shard_invariance():
         if k == "first_violation_tick":
             vals = [v for v in (cl[k], ch[k]) if v is not None]
             assert cw[k] == (min(vals) if vals else None)
+        elif k == "payload_max":
+            assert cw[k] == max(cl[k], ch[k])
         else:
             assert cw[k] == cl[k] + ch[k], k
 
@@ -163,6 +216,7 @@ def test_gpu_write_state_roundtrip():
     g = helpers.gpu(**cfg)
     r = helpers.oracle(**cfg)
     for be in (g, r):
+        be.set_tick(15000)                       # resume: deadlines are absolute ticks
         be.write_nodes(0, src.read_nodes_raw())
         be.write_clusters(0, src.read_clusters())
         for c in range(cfg["n_clusters"]):
@@ -171,9 +225,32 @@ def test_gpu_write_state_roundtrip():
                 for w in (0, 1):
                     be.write_queue(c, i, w, src.read_queue(c, i, w))
     assert np.array_equal(g.digest(), src.digest())
-    for be in (g, r):
+    for be in (g, r, src):
         be.step(8000)
     assert np.array_equal(g.digest(), r.digest())
+    assert np.array_equal(g.digest(), src.digest())     # resumed == never stopped
+
+
+def test_gpu_multi_launch_step():
+    """One raft_sim_step spanning several launches (ticks_per_launch < n_ticks) equals the oracle."""
+    cfg = dict(n_clusters=512, nodes=5, seed=81, client_ppm=20000, log_cap=64,
+               ticks_per_launch=3000, **BURSTS, **FAULTS)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    g.step(17000)
+    r.step(17000)
+    assert g.tick == r.tick == 17000
+    assert np.array_equal(g.digest(), r.digest()) and g.counters() == r.counters()
+
+
+def test_gpu_tick_horizon():
+    """No deadline or arrival may wrap past 2^32 (SIM_SPEC D1): steps that could are refused."""
+    g = helpers.gpu(n_clusters=64, nodes=5, seed=1)
+    top = 2 ** 32 - 1 - 10000        # the longest timer is el_base + el_span = 10000
+    g.set_tick(top - 3000)
+    g.step(2999)
+    with pytest.raises(helpers.RaftSimError, match="2\\^32"):
+        g.step(2)
+    g.step(0)
 
 
 @pytest.mark.gpu

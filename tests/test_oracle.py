@@ -37,6 +37,12 @@ def random_config(rng):
     if rng.random() < 0.5:
         cfg.update(part_ppm=rng.choice([50000, 300000]), part_epoch=rng.choice([100, 1000]))
     cfg["client_ppm"] = rng.choice([0, 100, 1000, 20000])
+    if cfg["client_ppm"] and rng.random() < 0.6:       # bursts + followed redirects (D14, D15)
+        cfg["client_redirects"] = rng.choice([0, 1, 2, 4, 16])
+        if rng.random() < 0.7:
+            period = rng.choice([7, 300, 2000, 16384])
+            cfg.update(client_period=period, client_burst=rng.randint(1, period),
+                       client_ppm=rng.choice([20000, 200000, 1000000]))
     if rng.random() < 0.5:
         cfg.update(hb=rng.randint(5, 300), el_base=rng.randint(5, 500), el_span=rng.randint(1, 500))
     if rng.random() < 0.2:
@@ -116,14 +122,36 @@ def test_spec_raft_is_safe_and_the_injected_bug_is_not(nodes):
     assert b["first_violation_tick"] is not None
 
 
-def test_message_conservation():
-    """sent + client_injected - dropped - partitioned + duplicated = delivered + overflow + to_halted."""
+@pytest.mark.parametrize("redirects", [0, 3])
+def test_message_conservation(redirects):
+    """sent + client_injected + redirects - dropped - partitioned + duplicated
+    = delivered + overflow + to_halted; every client-set a non-leader handles is either
+    re-sent along the redirect (redirects) or abandoned."""
     be = helpers.oracle(n_clusters=64, nodes=5, seed=5, drop_ppm=100000, dup_ppm=50000, dmax=20,
-                        part_ppm=100000, client_ppm=2000, inbox_cap=3, log_cap=64)
+                        part_ppm=100000, client_ppm=20000, inbox_cap=3, log_cap=64,
+                        client_period=4000, client_burst=800, client_redirects=redirects)
     be.step(20000)
     c = be.counters()
-    assert (c["sent"] + c["client_injected"] - c["dropped"] - c["partitioned"] + c["duplicated"]
-            == c["delivered"] + c["overflow"] + c["to_halted"])
+    assert (c["sent"] + c["client_injected"] + c["redirects"] - c["dropped"] - c["partitioned"]
+            + c["duplicated"] == c["delivered"] + c["overflow"] + c["to_halted"])
+    assert c["redirects"] > 0 if redirects else c["redirects"] == 0
+    assert c["client_abandoned"] > 0
+
+
+def test_client_schedule_bursts():
+    """D14: client-sets arrive only in the first client_burst ticks of every client_period."""
+    import pyref
+    P, B = 1000, 150
+    for j in range(0, 5000, 7):
+        t = pyref.on_tick(j, P, B)
+        assert t % P < B and pyref.on_index(t, P, B) == j
+    be = helpers.oracle(n_clusters=32, nodes=5, seed=3, client_ppm=300000, client_period=P,
+                        client_burst=B, trace_cap=4096)
+    be.step(6000)
+    ticks = [e["tick"] for c in range(32) for i in range(1, 6) for e in be.trace(c, i)
+             if (e["msg"]["hdr"] & 7) == 3 and e["msg"]["arrival"] == e["tick"]]
+    assert ticks and all(t % P < B for t in ticks)
+    assert be.counters()["client_injected"] > 0.2 * 32 * 6 * B
 
 
 def test_commit_logs_written_like_the_reference(tmp_path):
@@ -139,6 +167,21 @@ def test_commit_logs_written_like_the_reference(tmp_path):
     assert be.counters()["entries_applied"] == sum(r["commit_count"] for r in be.read_nodes())
 
 
+@pytest.mark.parametrize("variant", [0, 2])
+def test_idle_skipping_does_not_change_results(variant):
+    """The CPU baseline's discrete-event skipping visits only ticks with something due and gives
+    the every-tick restatement's results exactly."""
+    cfg = dict(n_clusters=61, nodes=5, seed=13, client_ppm=50000, drop_ppm=50000, dmax=30,
+               part_ppm=100000, log_cap=128, client_period=5000, client_burst=700,
+               client_redirects=3, variant_flags=variant, trace_cap=64, trace_entry_cap=512)
+    a, b = helpers.oracle(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_idle_skip(b)
+    for n in (1, 4999, 7000, 3):
+        a.step(n)
+        b.step(n)
+        assert (a.digest() == b.digest()).all() and a.counters() == b.counters()
+
+
 def test_threads_do_not_change_results():
     cfg = dict(n_clusters=97, nodes=7, seed=3, client_ppm=1000, drop_ppm=50000, dmax=9)
     a, b = helpers.oracle(**cfg), helpers.oracle(**cfg)
@@ -146,3 +189,49 @@ def test_threads_do_not_change_results():
     a.step(7000)
     b.step(7000)
     assert (a.digest() == b.digest()).all() and a.counters() == b.counters()
+
+
+def test_sharded_oracle_equals_single():
+    """n_devices = G splits the clusters into G independent shards (the product's multi-GPU
+    handle, include/raftsim.h); every G gives the same clusters, counters and routed reads."""
+    cfg = dict(n_clusters=203, nodes=5, seed=71, client_ppm=80000, log_cap=128,
+               client_period=3000, client_burst=600, client_redirects=4, **FAULTS)
+    one = helpers.oracle(**cfg)
+    one.step(9000)
+    for g in (2, 3, 8):
+        many = helpers.oracle(n_devices=g, **cfg)
+        many.step(9000)
+        assert (one.digest() == many.digest()).all()
+        assert one.counters() == many.counters()
+        assert one.read_nodes(60, 90) == many.read_nodes(60, 90)
+        assert one.read_clusters(0, 203) == many.read_clusters(0, 203)
+        for c in (0, 67, 68, 101, 202):
+            assert one.read_queue(c, 2, 0) == many.read_queue(c, 2, 0)
+            assert one.log(c, 3) == many.log(c, 3)
+
+
+def test_resume_and_tick_horizon():
+    """set_tick + the write_* calls resume a run exactly (deadlines are absolute ticks); steps
+    whose timers could reach 2^32 - 1 are refused (SIM_SPEC D1)."""
+    cfg = dict(n_clusters=16, nodes=5, seed=3, client_ppm=3000, log_cap=64, **FAULTS)
+    src = helpers.oracle(**cfg)
+    src.step(7000)
+    dst = helpers.oracle(**cfg)
+    dst.set_tick(7000)
+    dst.write_nodes(0, src.read_nodes_raw())
+    dst.write_clusters(0, src.read_clusters())
+    for c in range(16):
+        for i in range(1, 6):
+            dst.write_arena(c, i, src.read_arena(c, i))
+            for w in (0, 1):
+                dst.write_queue(c, i, w, src.read_queue(c, i, w))
+    for be in (src, dst):
+        be.step(5000)
+    assert (src.digest() == dst.digest()).all()
+    top = 2 ** 32 - 1 - 10000
+    src.set_tick(top - 100)
+    src.step(99)
+    with pytest.raises(helpers.RaftSimError, match="2\\^32"):
+        src.step(2)
+    with pytest.raises(helpers.RaftSimError):
+        src.set_tick(top + 5)
