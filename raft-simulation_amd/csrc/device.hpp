@@ -18,6 +18,10 @@
 
 namespace rs {
 
+#ifndef RS_PHILOX_MAD
+#define RS_PHILOX_MAD 0
+#endif
+
 constexpr uint32_t INF = 0xFFFFFFFFu;
 enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
@@ -48,19 +52,36 @@ struct DevSim {
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
   unsigned long long* ctr;  // [RAFT_CTR_COUNT] sums, [+0] first violation (min), [+1] payload (max)
-  const uint32_t* perm;     // [C] wave slot -> cluster (RAFT_SCHED_ALIGNED), null = identity
+  const uint32_t* perm;     // [slots] wave slot -> cluster or INF (RAFT_SCHED_ALIGNED), null = identity
+  const uint32_t* nslots;   // RAFT_SCHED_ALIGNED: slots in use this launch (device word)
   uint32_t* skey;           // [C] RAFT_SCHED_ALIGNED: cluster's next event - next launch's t0
   uint32_t* shist;          // [SCHED_BUCKETS] histogram of skey (null: schedule fixed)
+  uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
 };
 constexpr uint32_t SCHED_BUCKETS = 16384;   // keys clamp to SCHED_BUCKETS - 1
+constexpr uint32_t SCHED_PAST = 16;         // bucket of "now": keys keep 16 ticks of past
+
+// Slots the padded wave packing may use (RAFT_SCHED_ALIGNED): twice the clusters, plus one partial
+// wave per plan chunk; the tick kernel's grid covers this many and waves past the slots in use exit.
+__host__ __device__ inline uint32_t sched_slots_bound(uint32_t C, uint32_t N) {
+  const uint32_t CPW = 64 / N;
+  return ((2 * C + CPW - 1) / CPW + 256 + 1) * CPW;
+}
 
 // Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).
 __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
+#if RS_PHILOX_MAD
+    // one 32x32->64 product (v_mad_u64_u32) gives both halves
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
     const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+#endif
     c0 = hi1 ^ c1 ^ k0;
     c1 = lo1;
     c2 = hi0 ^ c3 ^ k1;

@@ -11,7 +11,8 @@
 namespace rs {
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
-hipError_t launch_sched_perm(const DevSim& S, uint32_t* off, uint32_t* perm, hipStream_t st);
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* plan,
+                             uint32_t* nslots, hipStream_t st);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -55,7 +56,7 @@ struct Shard {
   // d.skey/d.shist hold a matching key set (from the previous tick launch). Only the first launch
   // computes them from the state: after host writes the keys are merely stale, which changes the
   // packing (speed), never the results.
-  uint32_t *soff, *sperm;
+  uint32_t *soff, *sperm, *splan, *snslots;   // + per-bucket plan [SCHED_BUCKETS + 256], slot count
   bool keys_fresh;
 };
 
@@ -179,9 +180,18 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     return rc;
   }
   d.client_pw = s->client_pw;
+  d.wavelog = nullptr;
+#ifdef RS_WAVELOG
+  if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {
+    sh_destroy(s);
+    return rc;
+  }
+#endif
   if (cfg->schedule == RAFT_SCHED_ALIGNED) {
     if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
-        (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) || (rc = dalloc(s, &s->sperm, s->C))) {
+        (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) ||
+        (rc = dalloc(s, &s->sperm, rs::sched_slots_bound(s->C, s->N))) ||
+        (rc = dalloc(s, &s->splan, rs::SCHED_BUCKETS + 256)) || (rc = dalloc(s, &s->snslots, 1))) {
       sh_destroy(s);
       return rc;
     }
@@ -232,10 +242,11 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       // pack clusters with the same next event onto the same waves for this launch: keys and
       // histogram come from the previous tick launch, or are recomputed from the state
       if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->stream));
+      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->splan, s->snslots, s->stream));
       // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
       std::swap(s->d.shist, s->soff);
       s->d.perm = s->sperm;
+      s->d.nslots = s->snslots;
       s->keys_fresh = true;
     }
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
@@ -243,6 +254,10 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       HIP_OK(hipEventCreate(&e));
       s->kev.push_back(e);
     }
+#ifdef RS_WAVELOG
+    HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
+                          (size_t)rs::sched_slots_bound(s->C, s->N) * 32 / (64 / s->N), s->stream));
+#endif
     HIP_OK(hipEventRecord(s->kev[2 * launches], s->stream));
     HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
     HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
@@ -852,3 +867,17 @@ int raft_sim_read_counters(raft_sim_t* r, raft_counters_t* out) {
   }
   return 0;
 }
+
+#ifdef RS_WAVELOG
+// Diagnostic builds only (not part of include/raftsim.h): the per-wave timeline of shard 0's last
+// tick-kernel launch, 8 words per wave: start lo/hi, end lo/hi (100 MHz), active ticks, HW_ID,
+// XCC_ID, launch t0. Returns the number of waves.
+extern "C" int raftsim_diag_wavelog(raft_sim_t* r, uint32_t* out, uint32_t cap_waves) {
+  Shard* s = r->sh[0];
+  const uint32_t waves = rs::sched_slots_bound(s->C, s->N) / (64 / s->N);
+  const uint32_t n = std::min(waves, cap_waves);
+  HIP_OK(hipSetDevice(s->cfg.device));
+  HIP_OK(hipMemcpy(out, s->d.wavelog, (size_t)n * 32, hipMemcpyDeviceToHost));
+  return (int)n;
+}
+#endif

@@ -335,8 +335,11 @@ template <int N>
 constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 // NM_LDS: the wave's next_index / match_index rows live in LDS during a launch ([2][N][64]
 // words), for the N whose block then still fits four per CU.
+#ifndef RS_NM_LDS
+#define RS_NM_LDS 1
+#endif
 template <int N>
-constexpr bool nm_lds() { return N <= 5; }
+constexpr bool nm_lds() { return RS_NM_LDS && N <= 5; }
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0);
@@ -353,6 +356,23 @@ constexpr size_t block_lds_bytes() {
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
 #endif
+
+// RAFT_SCHED_ALIGNED packing key of a node: its next event (deadline or queue head).
+__device__ __forceinline__ uint32_t sched_key_of(uint32_t deadline, const QueueR& rq,
+                                                 const QueueR& rs) {
+  return min(deadline, min(rq.arr, rs.arr));
+}
+// The histogram bucket of a cluster whose next event is `ev`, for a launch starting at t0. Events
+// up to SCHED_PAST ticks in the past (messages that arrived but wait behind others, e.g. a
+// leader's remaining append-responses in mid round) keep their tick: they tell a cluster that is
+// 3 ticks into a heartbeat round from one that starts a round at t0, whose later rounds would
+// otherwise stay 3 ticks apart in the same wave.
+__device__ __forceinline__ uint32_t sched_bucket(uint32_t ev, uint32_t t0) {
+  const uint64_t k = (uint64_t)ev + SCHED_PAST;
+  if (k <= t0) return 0;
+  const uint64_t d = k - t0;
+  return d < SCHED_BUCKETS - 1 ? (uint32_t)d : SCHED_BUCKETS - 1;
+}
 
 template <int N, bool TRACE, bool SPEC>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
@@ -373,10 +393,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   __builtin_amdgcn_wave_barrier();
 
   const uint32_t wave = blockIdx.x;
+  // RAFT_SCHED_ALIGNED launches a grid sized for the padded packing; waves past its slots exit
+  const uint32_t nslots = S.perm ? *S.nslots : S.C;
+  if (wave * CPW >= nslots) return;
   const int cs = lane / N, k0 = lane - cs * N;
   const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
-  const bool active = lane < CPW * N && slot < S.C;
-  const uint32_t c = active && S.perm ? S.perm[slot] : slot;
+  const uint32_t c0 = lane < CPW * N && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
+  const bool active = c0 != INF;
+  const uint32_t c = active ? c0 : 0u;
   const uint32_t gi = c * N + k0;
   const uint32_t g = S.goff + c;
   const int bl0 = (cs < CPW ? cs : 0) * N;     // the cluster's first lane
@@ -414,6 +438,16 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
+#ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
+  const uint64_t wl_start = wall_clock64();
+  uint32_t wl_active = 0, wl_first = INF;
+  uint32_t wl_kmin = INF, wl_kmax = 0;
+  {
+    const uint32_t key = (active && k0 == 0 && S.skey) ? S.skey[c] : INF;
+    wl_kmin = wave_min(key);
+    wl_kmax = ~wave_min(key == INF ? ~0u : ~key);
+  }
+#endif
 
   const uint32_t tend = t0 + nt;
   for (uint32_t t = t0;; ++t) {
@@ -1042,19 +1076,34 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
     wnext = next_event();
+#ifdef RS_WAVELOG
+    ++wl_active;
+    wl_first = wl_first == INF ? t - t0 : wl_first;
+#endif
   }
+#ifdef RS_WAVELOG
+  if (lane == 0 && S.wavelog) {
+    const uint64_t wl_end = wall_clock64();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 8);
+    rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
+                        (uint32_t)(wl_end >> 32));
+    rec[1] = make_uint4(wl_active, hw, xcc, (wl_kmax - wl_kmin) << 16 | (wl_first & 0xFFFF));
+  }
+#endif
 
   // ---------------------------------------------------------------- write back
   if (S.shist) {
-    // RAFT_SCHED_ALIGNED: the cluster's next event relative to the next launch, counted into the
+    // RAFT_SCHED_ALIGNED: the cluster's packing key relative to the next launch, counted into the
     // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
-    const uint32_t me = active && !n.fault ? min(n.deadline, min(n.rq.arr, n.rs.arr)) : INF;
+    const uint32_t me = active && !n.fault ? sched_key_of(n.deadline, n.rq, n.rs) : INF;
     uint32_t cm = active ? cnext : INF;
 #pragma unroll
     for (int s = 0; s < N; ++s) cm = min(cm, (uint32_t)__shfl(me, bl0 + s));
     if (active && k0 == 0) {
-      const uint32_t d = cm > tend ? cm - tend : 0u;
-      const uint32_t key = d < SCHED_BUCKETS - 1 ? d : SCHED_BUCKETS - 1;
+      const uint32_t key = sched_bucket(cm, tend);
       S.skey[c] = key;
       atomicAdd(&S.shist[key], 1u);
     }
@@ -1109,61 +1158,104 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   for (uint32_t k = 0; k < S.N; ++k) {
     const uint32_t gi = c * S.N + k;
     if ((S.flags[gi] >> 10) & 7) continue;
-    m = min(m, min(S.deadline[gi], min(S.req_arr[gi], S.res_arr[gi])));
+    const uint32_t qm = S.qmeta[gi];
+    const QueueR rq = {0, (qm >> 4) & 31, S.req_arr[gi], 0}, rs = {0, (qm >> 13) & 31, S.res_arr[gi], 0};
+    m = min(m, sched_key_of(S.deadline[gi], rq, rs));
   }
-  const uint32_t d = m > t0 ? m - t0 : 0u;
-  const uint32_t key = d < SCHED_BUCKETS - 1 ? d : SCHED_BUCKETS - 1;
+  const uint32_t key = sched_bucket(m, t0);
   S.skey[c] = key;
   atomicAdd(&S.shist[key], 1u);
 }
 
-// Scan + scatter without global atomics: block b of SCHED_RANGE_BLOCKS owns the key range
-// [b*KB, (b+1)*KB). It sums the histogram below its range (its base), scans its own KB buckets
-// into LDS offsets, then reads every cluster's key and places the clusters of its range with LDS
-// atomics. Each block reads all keys (L2-resident, 4 B per cluster); 13 us per launch at C2 (a
-// separate scan and a device-atomic scatter took 22.5 us). The histogram is double-buffered: this kernel reads S.shist and zeroes `zero`,
-// which the next tick launch fills (the host swaps the two).
+// Window-limited packing (plan, then place). Clusters are taken in key order, but a wave never
+// holds keys more than SCHED_WINDOW ticks apart: where the keys are sparse (the first elections
+// bunch near el_base, so some phases hold one cluster per tick) a wave is closed early and padded
+// instead of mixing up to ten phases, whose rounds would all be active ticks of the wave (C2: the
+// slowest wave 60 -> 34 active ticks for ~4 % more waves, measured offline against the oracle).
+//
+// sched_plan_kernel (one block of SCHED_CHUNKS threads): thread j walks the SCHED_CHUNK buckets
+// of chunk j (a fresh window at every chunk start) and gives each bucket its first slot relative
+// to the chunk, padding where the window closes a wave; chunk totals are whole waves. If the
+// padded total would exceed the grid bound (sched_slots_bound), every chunk falls back to the
+// plain counting sort (no padding).
+constexpr uint32_t SCHED_CHUNK = 64;
+constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 256
 constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
+constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets = 4 chunks
+constexpr uint32_t SCHED_WINDOW = 1;
+
+template <uint32_t CPW>
+__device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t* st, bool window) {
+  uint32_t slot = 0, f = 0;                           // f = slot % CPW
+  int kw = -(int)SCHED_CHUNK;                         // bucket where the open wave began
+#pragma unroll
+  for (uint32_t i = 0; i < SCHED_CHUNK; ++i) {
+    const uint32_t n = cnt[i];
+    if (window && n && f && (int)i > kw + (int)SCHED_WINDOW) {
+      slot += CPW - f;                                // close the open wave, pad its tail
+      f = 0;
+    }
+    if (st) st[i] = slot;
+    if (n && (f == 0 || f + n > CPW)) kw = (int)i;    // the wave open after this bucket began here
+    slot += n;
+    f = (f + n) % CPW;
+  }
+  return slot + (f ? CPW - f : 0);
+}
+
+template <uint32_t CPW>
+__global__ void __launch_bounds__(SCHED_CHUNKS) sched_plan_kernel(DevSim S, uint32_t* start,
+                                                                  uint32_t* total) {
+  __shared__ uint32_t wsum[SCHED_CHUNKS / 64];
+  const uint32_t j = threadIdx.x, lane = j & 63;
+  uint32_t cnt[SCHED_CHUNK];
+  const uint4* h4 = reinterpret_cast<const uint4*>(S.shist + j * SCHED_CHUNK);
+#pragma unroll
+  for (uint32_t i = 0; i < SCHED_CHUNK / 4; ++i) {
+    const uint4 v = h4[i];
+    cnt[4 * i] = v.x; cnt[4 * i + 1] = v.y; cnt[4 * i + 2] = v.z; cnt[4 * i + 3] = v.w;
+  }
+  uint32_t sum = plan_chunk<CPW>(cnt, nullptr, true);   // block total of the padded plan
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
+  if (lane == 0) wsum[j >> 6] = sum;
+  __syncthreads();
+  uint32_t all = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < SCHED_CHUNKS / 64; ++w) all += wsum[w];
+  const bool window = all <= sched_slots_bound(S.C, 64 / CPW) - SCHED_CHUNKS * CPW;
+  total[j] = plan_chunk<CPW>(cnt, start + j * SCHED_CHUNK, window);
+}
+
+// sched_range_kernel: block b sums the slot totals of the ranges below its own (its base), marks
+// its slots empty, then reads every cluster's key and places the clusters of its range at
+// base + start[bucket] + rank (LDS atomics, no global ones). Each block reads all keys
+// (L2-resident, 4 B per cluster). The histogram is double-buffered: this kernel reads S.shist
+// (via the plan) and zeroes `zero`, which the next tick launch fills (the host swaps the two).
+// The last block publishes the slot count the tick kernel's grid covers.
 __global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* zero,
-                                                           uint32_t* perm) {
-  constexpr uint32_t KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;   // 256
+                                                           uint32_t* perm, const uint32_t* start,
+                                                           const uint32_t* total,
+                                                           uint32_t* nslots) {
+  constexpr uint32_t KB = SCHED_KB;
   static_assert(KB <= 1024 && KB % 64 == 0, "one thread per bucket of the range");
   __shared__ uint32_t loff[KB];
-  __shared__ uint32_t wsum[16];
-  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t t = threadIdx.x;
   const uint32_t k0 = blockIdx.x * KB;
   if (t < KB) zero[k0 + t] = 0;
-  uint32_t part = 0;                                  // buckets below the range, 16 loads in flight
-#pragma unroll
-  for (uint32_t i = 0; i < SCHED_BUCKETS / 1024; ++i) {
-    const uint32_t idx = t * (SCHED_BUCKETS / 1024) + i;
-    part += idx < k0 ? S.shist[idx] : 0u;
-  }
-  const uint32_t mine = t < KB ? S.shist[k0 + t] : 0u;
-  // block sum of `part` (wave reduce, then 16 wave totals)
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d);
-  if (lane == 0) wsum[w] = part;
-  // exclusive scan of `mine` over the KB range threads (waves 0..KB/64-1)
-  uint32_t inc = mine;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t x = __shfl_up(inc, d);
-    if (lane >= d) inc += x;
-  }
-  __syncthreads();
+  constexpr uint32_t CPB = KB / SCHED_CHUNK;           // chunks per block
   uint32_t base = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < 16; ++j) base += wsum[j];
-  __syncthreads();
-  if (t < KB && lane == 63) wsum[w] = inc;            // range-wave totals (w < KB / 64)
-  __syncthreads();
+  for (uint32_t j = 0; j < blockIdx.x * CPB; ++j) base += total[j];
+  uint32_t mine = 0;
+  for (uint32_t j = 0; j < CPB; ++j) mine += total[blockIdx.x * CPB + j];
   if (t < KB) {
-    uint32_t run = base + inc - mine;
-    for (uint32_t j = 0; j < w; ++j) run += wsum[j];
-    loff[t] = run;
+    uint32_t cb = base;                                 // base of this bucket's chunk
+    for (uint32_t j = 0; j < t / SCHED_CHUNK; ++j) cb += total[blockIdx.x * CPB + j];
+    loff[t] = cb + start[k0 + t];
   }
-  __syncthreads();
+  for (uint32_t i = t; i < mine; i += 1024) perm[base + i] = INF;
+  if (blockIdx.x == SCHED_RANGE_BLOCKS - 1 && t == 0) *nslots = base + mine;
+  __syncthreads();                      // the empty marks land before the placements
   // keys as 16-byte vectors, sixteen loads in flight per thread (64 keys), then the scalar tail
   const uint32_t C4 = S.C / 4;
   const uint4* k4 = reinterpret_cast<const uint4*>(S.skey);
@@ -1195,9 +1287,21 @@ hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, hipStream_t st) {
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* plan,
+                             uint32_t* nslots, hipStream_t st) {
+  uint32_t* total = plan + SCHED_BUCKETS;
+  switch (64 / S.N) {
+#define RS_PLAN(CPW)                                                                           \
+  case CPW:                                                                                    \
+    hipLaunchKernelGGL(sched_plan_kernel<CPW>, dim3(1), dim3(SCHED_CHUNKS), 0, st, S, plan,    \
+                       total);                                                                 \
+    break;
+    RS_PLAN(32) RS_PLAN(21) RS_PLAN(16) RS_PLAN(12) RS_PLAN(10) RS_PLAN(9) RS_PLAN(8) RS_PLAN(7)
+#undef RS_PLAN
+    default: return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(sched_range_kernel, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, zero,
-                     perm);
+                     perm, plan, total, nslots);
   return hipGetLastError();
 }
 
@@ -1292,7 +1396,7 @@ template <int N, bool SPEC>
 void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
   constexpr int CPW = 64 / N;
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
-  const uint32_t waves = (S.C + CPW - 1) / CPW;
+  const uint32_t waves = S.perm ? sched_slots_bound(S.C, N) / CPW : (S.C + CPW - 1) / CPW;
   if (S.TC)
     hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(waves), dim3(64), lds, st, S, t0, nt);
   else

@@ -11,10 +11,13 @@ sys.path[:0] = [str(ROOT / "raft-simulation_amd")]
 from raftsim._backend import Backend  # noqa: E402
 
 FAULTS = dict(drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
+BURSTS = dict(client_period=16384, client_burst=2048, client_redirects=4)
 WORK = {
     "c2": dict(n_clusters=65536, nodes=5, seed=42),
-    "c3": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=10000, log_cap=256, **FAULTS),
-    "c4_n9": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=250000, log_cap=4096),
+    "c3": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=80000, log_cap=256, **BURSTS,
+               **FAULTS),
+    "c4_n9": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=500000, log_cap=4096,
+                  client_period=8192, client_burst=2048, client_redirects=4),
 }
 
 

@@ -1,0 +1,63 @@
+"""Per-wave timeline of one C2 launch from a -DRS_WAVELOG build (diagnostic only): lifetime
+distribution, start-time generations, per-CU/SIMD packing. Usage: wavelog_probe.py LIB [clusters]"""
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "raft-simulation_amd")]
+from raftsim._backend import Backend  # noqa: E402
+
+lib = sys.argv[1]
+C = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+sim = Backend(lib, "raft_sim_", n_clusters=C, nodes=5, seed=42)
+sim.step(10000)
+sim.step(10000)
+waves = 2 * C // 12 + 1000                     # >= the padded packing's grid
+buf = (ctypes.c_uint32 * (waves * 8))()
+n = sim._lib.raftsim_diag_wavelog(sim._h, buf, waves)
+a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 8)[:n].astype(np.int64)
+a = a[(a[:, 0] | a[:, 1]) != 0]                 # waves that ran (padding waves exit first)
+n = len(a)
+start = (a[:, 0] | (a[:, 1] << 32)); end = (a[:, 2] | (a[:, 3] << 32))
+t0 = start.min()
+st, en = (start - t0) / 100.0, (end - t0) / 100.0        # microseconds
+life = en - st
+act = a[:, 4]
+hw, xcc = a[:, 5], a[:, 6]
+simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) & 7
+print(f"kernel_ms {sim.last_step_timing()[0]:.3f} waves {n}  span {en.max():.1f} us")
+q = lambda x: " ".join(f"{v:7.1f}" for v in np.percentile(x, [0, 10, 50, 90, 99, 100]))
+print("life  us p0/10/50/90/99/100:", q(life))
+print("start us p0/10/50/90/99/100:", q(st))
+print("end   us p0/10/50/90/99/100:", q(en))
+print("active ticks p0/10/50/90/99/100:", q(act))
+print("us per active tick p0/10/50/90/99/100:", q(life / np.maximum(act, 1)))
+for lo, hi in ((0, 5), (5, 40), (40, 100), (100, 1e9)):
+    m = (st >= lo) & (st < hi)
+    if m.any():
+        print(f"started [{lo},{hi}) us: {m.sum():5d} waves, life median {np.median(life[m]):6.1f} us, "
+              f"active median {np.median(act[m]):5.1f}, end max {en[m].max():6.1f}")
+kspread, first = a[:, 7] >> 16, a[:, 7] & 0xFFFF
+print("key spread in wave p0/10/50/90/99/100:", q(kspread))
+print("first active tick p0/10/50/90/99/100:", q(first))
+for lo_a in (18, 25, 35, 50):
+    m = act >= lo_a
+    print(f"waves with >= {lo_a} active: {m.sum():5d}  key spread median {np.median(kspread[m]) if m.any() else 0}"
+          f"  first tick median {np.median(first[m]) if m.any() else 0}")
+slow = life > np.percentile(life, 90)
+print("slowest 10%: active median", np.median(act[slow]), "start median", np.median(st[slow]),
+      "index median", np.median(np.nonzero(slow)[0]))
+key = xcc * 10000 + se * 1000 + sh * 100 + cu * 4 + simd
+u, cnt = np.unique(key, return_counts=True)
+print("distinct SIMDs", len(u), "waves per SIMD p0/50/100", cnt.min(), np.median(cnt), cnt.max())
+busy = {}
+for k in u:
+    m = key == k
+    busy[k] = life[m].sum()
+b = np.array(list(busy.values()))
+print("per-SIMD summed wave-us p0/50/100:", b.min(), np.median(b), b.max())
+per_xcc = [np.median(life[xcc == x]) for x in range(8)]
+print("per-XCC median life:", " ".join(f"{v:.1f}" for v in per_xcc))
