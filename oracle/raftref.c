@@ -1102,7 +1102,7 @@ static int sh_read_queue(shard_t* s, uint32_t cluster, uint32_t id, uint32_t whi
   raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
   uint32_t cnt = which ? n->res_count : n->req_count;
   uint32_t m = cnt < cap ? cnt : cap;
-  memcpy(out, qslot(s, cluster * s->N + id - 1, (int)which), m * sizeof(raft_msg_t));
+  if (out && m) memcpy(out, qslot(s, cluster * s->N + id - 1, (int)which), m * sizeof(raft_msg_t));
   return (int)cnt;
 }
 
@@ -1121,7 +1121,7 @@ static int sh_write_queue(shard_t* s, uint32_t cluster, uint32_t id, uint32_t wh
   }
   raft_msg_t* q = qslot(s, cluster * s->N + id - 1, (int)which);
   memset(q, 0, s->Q * sizeof *q);
-  memcpy(q, in, count * sizeof *q);
+  if (count) memcpy(q, in, count * sizeof *q);
   raft_node_t* n = &s->nodes[(size_t)cluster * s->N + id - 1];
   if (which) n->res_count = count; else n->req_count = count;
   return 0;
@@ -1132,7 +1132,7 @@ static int sh_read_arena(shard_t* s, uint32_t cluster, uint32_t id, raft_entry_t
   int rc = check_node(s, cluster, id);
   if (rc) return rc;
   uint32_t m = cap < s->A ? cap : s->A;
-  memcpy(out, arena_of(s, cluster * s->N + id - 1), m * sizeof(raft_entry_t));
+  if (out && m) memcpy(out, arena_of(s, cluster * s->N + id - 1), m * sizeof(raft_entry_t));
   return (int)s->A;
 }
 
@@ -1143,7 +1143,7 @@ static int sh_write_arena(shard_t* s, uint32_t cluster, uint32_t id, const raft_
   if (count > s->A) return fail(-EINVAL, "count > arena_cap");
   raft_entry_t* a = arena_of(s, cluster * s->N + id - 1);
   memset(a, 0, s->A * sizeof *a);
-  memcpy(a, in, count * sizeof *a);
+  if (count) memcpy(a, in, count * sizeof *a);
   return 0;
 }
 

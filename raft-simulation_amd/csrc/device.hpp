@@ -61,11 +61,13 @@ struct DevSim {
 constexpr uint32_t SCHED_BUCKETS = 16384;   // keys clamp to SCHED_BUCKETS - 1
 constexpr uint32_t SCHED_PAST = 16;         // bucket of "now": keys keep 16 ticks of past
 
-// Slots the padded wave packing may use (RAFT_SCHED_ALIGNED): twice the clusters, plus one partial
-// wave per plan chunk; the tick kernel's grid covers this many and waves past the slots in use exit.
+// Slots the padded wave packing may use (RAFT_SCHED_ALIGNED): twice the clusters plus one partial
+// wave per plan chunk (SCHED_PLAN_CHUNKS), so the unpadded fallback always fits; the tick kernel's
+// grid covers this many and waves past the slots in use exit at once.
+constexpr uint32_t SCHED_PLAN_CHUNKS = 1024;
 __host__ __device__ inline uint32_t sched_slots_bound(uint32_t C, uint32_t N) {
   const uint32_t CPW = 64 / N;
-  return ((2 * C + CPW - 1) / CPW + 256 + 1) * CPW;
+  return ((2 * C + CPW - 1) / CPW + SCHED_PLAN_CHUNKS) * CPW;
 }
 
 // Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).

@@ -9,10 +9,11 @@
 #include "device.hpp"
 
 namespace rs {
-hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st);
+hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
+                       hipEvent_t ev1);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
-hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* plan,
-                             uint32_t* nslots, hipStream_t st);
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
+                             hipStream_t st);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -56,7 +57,7 @@ struct Shard {
   // d.skey/d.shist hold a matching key set (from the previous tick launch). Only the first launch
   // computes them from the state: after host writes the keys are merely stale, which changes the
   // packing (speed), never the results.
-  uint32_t *soff, *sperm, *splan, *snslots;   // + per-bucket plan [SCHED_BUCKETS + 256], slot count
+  uint32_t *soff, *sperm, *snslots;   // + the slot count of the packing
   bool keys_fresh;
 };
 
@@ -191,7 +192,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
         (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) ||
         (rc = dalloc(s, &s->sperm, rs::sched_slots_bound(s->C, s->N))) ||
-        (rc = dalloc(s, &s->splan, rs::SCHED_BUCKETS + 256)) || (rc = dalloc(s, &s->snslots, 1))) {
+        (rc = dalloc(s, &s->snslots, 1))) {
       sh_destroy(s);
       return rc;
     }
@@ -242,7 +243,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       // pack clusters with the same next event onto the same waves for this launch: keys and
       // histogram come from the previous tick launch, or are recomputed from the state
       if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->splan, s->snslots, s->stream));
+      HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream));
       // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
       std::swap(s->d.shist, s->soff);
       s->d.perm = s->sperm;
@@ -258,9 +259,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
                           (size_t)rs::sched_slots_bound(s->C, s->N) * 32 / (64 / s->N), s->stream));
 #endif
-    HIP_OK(hipEventRecord(s->kev[2 * launches], s->stream));
-    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream));
-    HIP_OK(hipEventRecord(s->kev[2 * launches + 1], s->stream));
+    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1]));
     done += nt;
     s->tick += nt;
     s->ticks_run += nt;

@@ -6,6 +6,8 @@
 // LDS cells, then — only when some lane of the wave did something — the wave runs the network
 // (P2), log transfer (P3) and checker (P4) phases of SIM_SPEC.md §4. Idle ticks cost a handful of
 // VALU instructions and one ballot.
+#include <hip/hip_ext.h>
+
 #include "device.hpp"
 
 namespace rs {
@@ -438,6 +440,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
+#ifdef RS_PRIO   // experiment: waves that have run many active ticks issue first on their SIMD
+  uint32_t nact = 0;
+#endif
 #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
   const uint64_t wl_start = wall_clock64();
   uint32_t wl_active = 0, wl_first = INF;
@@ -1076,6 +1081,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
     wnext = next_event();
+#ifdef RS_PRIO
+    ++nact;
+    if (nact == RS_PRIO) __builtin_amdgcn_s_setprio(1);
+    if (nact == RS_PRIO + 4) __builtin_amdgcn_s_setprio(2);
+    if (nact == RS_PRIO + 8) __builtin_amdgcn_s_setprio(3);
+#endif
 #ifdef RS_WAVELOG
     ++wl_active;
     wl_first = wl_first == INF ? t - t0 : wl_first;
@@ -1167,25 +1178,27 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   atomicAdd(&S.shist[key], 1u);
 }
 
-// Window-limited packing (plan, then place). Clusters are taken in key order, but a wave never
-// holds keys more than SCHED_WINDOW ticks apart: where the keys are sparse (the first elections
-// bunch near el_base, so some phases hold one cluster per tick) a wave is closed early and padded
-// instead of mixing up to ten phases, whose rounds would all be active ticks of the wave (C2: the
-// slowest wave 60 -> 34 active ticks for ~4 % more waves, measured offline against the oracle).
+// Window-limited packing. Clusters are taken in key order, but a wave never holds keys more than
+// SCHED_WINDOW ticks apart: where the keys are sparse (the first elections bunch near el_base, so
+// some phases hold one cluster per tick) a wave is closed early and padded instead of mixing up
+// to ten phases, whose rounds would all be active ticks of the wave (C2: the slowest wave 60 -> 34
+// active ticks for ~5 % more waves, measured offline against the oracle; tick kernel -24 %).
 //
-// sched_plan_kernel (one block of SCHED_CHUNKS threads): thread j walks the SCHED_CHUNK buckets
-// of chunk j (a fresh window at every chunk start) and gives each bucket its first slot relative
-// to the chunk, padding where the window closes a wave; chunk totals are whole waves. If the
-// padded total would exceed the grid bound (sched_slots_bound), every chunk falls back to the
-// plain counting sort (no padding).
-constexpr uint32_t SCHED_CHUNK = 64;
-constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 256
+// The window is planned per chunk of SCHED_CHUNK buckets, one thread each, restarting at every
+// chunk (16-bucket chunks cost ~1 % more waves than one serial walk); chunk totals are whole
+// waves. If the padded plan would exceed the grid bound (sched_slots_bound), every chunk falls
+// back to the plain counting sort.
+constexpr uint32_t SCHED_CHUNK = 16;
+constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 1024, one per thread
+static_assert(SCHED_CHUNKS == SCHED_PLAN_CHUNKS, "grid bound covers one partial wave per chunk");
 constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
-constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets = 4 chunks
+constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets per block
 constexpr uint32_t SCHED_WINDOW = 1;
+static_assert(SCHED_CHUNKS == 1024 && SCHED_KB % SCHED_CHUNK == 0, "one chunk per thread");
 
 template <uint32_t CPW>
-__device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t* st, bool window) {
+__device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t (&st)[SCHED_CHUNK],
+                               bool window) {
   uint32_t slot = 0, f = 0;                           // f = slot % CPW
   int kw = -(int)SCHED_CHUNK;                         // bucket where the open wave began
 #pragma unroll
@@ -1195,7 +1208,7 @@ __device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t* st,
       slot += CPW - f;                                // close the open wave, pad its tail
       f = 0;
     }
-    if (st) st[i] = slot;
+    st[i] = slot;
     if (n && (f == 0 || f + n > CPW)) kw = (int)i;    // the wave open after this bucket began here
     slot += n;
     f = (f + n) % CPW;
@@ -1203,58 +1216,75 @@ __device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t* st,
   return slot + (f ? CPW - f : 0);
 }
 
+// One launch: every block plans all chunks from the histogram (L2-resident, 64 KiB), scans the
+// chunk totals, and places the clusters of its own 256-bucket range at their bucket's slot plus
+// their rank (LDS atomics, no global ones). It first marks its slots empty (padding reads INF).
+// Each block reads all keys (L2-resident, 4 B per cluster). The histogram is double-buffered: this
+// kernel reads S.shist and zeroes `zero`, which the next tick launch fills (the host swaps the
+// two). Block 0 publishes the slot count the tick kernel's grid covers.
 template <uint32_t CPW>
-__global__ void __launch_bounds__(SCHED_CHUNKS) sched_plan_kernel(DevSim S, uint32_t* start,
-                                                                  uint32_t* total) {
-  __shared__ uint32_t wsum[SCHED_CHUNKS / 64];
-  const uint32_t j = threadIdx.x, lane = j & 63;
-  uint32_t cnt[SCHED_CHUNK];
-  const uint4* h4 = reinterpret_cast<const uint4*>(S.shist + j * SCHED_CHUNK);
+__global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* zero,
+                                                           uint32_t* perm, uint32_t* nslots) {
+  constexpr uint32_t KB = SCHED_KB;
+  __shared__ uint32_t cbase[SCHED_CHUNKS + 1];
+  __shared__ uint32_t loff[KB];
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t k0 = blockIdx.x * KB;
+  if (t < KB) zero[k0 + t] = 0;
+  uint32_t cnt[SCHED_CHUNK], st[SCHED_CHUNK];
+  const uint4* h4 = reinterpret_cast<const uint4*>(S.shist + t * SCHED_CHUNK);
 #pragma unroll
   for (uint32_t i = 0; i < SCHED_CHUNK / 4; ++i) {
     const uint4 v = h4[i];
     cnt[4 * i] = v.x; cnt[4 * i + 1] = v.y; cnt[4 * i + 2] = v.z; cnt[4 * i + 3] = v.w;
   }
-  uint32_t sum = plan_chunk<CPW>(cnt, nullptr, true);   // block total of the padded plan
+  uint32_t tot = plan_chunk<CPW>(cnt, st, true);
+  // exclusive scan of the chunk totals: wave scan, then the 16 wave totals
+  uint32_t inc = tot;
 #pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-  if (lane == 0) wsum[j >> 6] = sum;
-  __syncthreads();
-  uint32_t all = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < SCHED_CHUNKS / 64; ++w) all += wsum[w];
-  const bool window = all <= sched_slots_bound(S.C, 64 / CPW) - SCHED_CHUNKS * CPW;
-  total[j] = plan_chunk<CPW>(cnt, start + j * SCHED_CHUNK, window);
-}
-
-// sched_range_kernel: block b sums the slot totals of the ranges below its own (its base), marks
-// its slots empty, then reads every cluster's key and places the clusters of its range at
-// base + start[bucket] + rank (LDS atomics, no global ones). Each block reads all keys
-// (L2-resident, 4 B per cluster). The histogram is double-buffered: this kernel reads S.shist
-// (via the plan) and zeroes `zero`, which the next tick launch fills (the host swaps the two).
-// The last block publishes the slot count the tick kernel's grid covers.
-__global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* zero,
-                                                           uint32_t* perm, const uint32_t* start,
-                                                           const uint32_t* total,
-                                                           uint32_t* nslots) {
-  constexpr uint32_t KB = SCHED_KB;
-  static_assert(KB <= 1024 && KB % 64 == 0, "one thread per bucket of the range");
-  __shared__ uint32_t loff[KB];
-  const uint32_t t = threadIdx.x;
-  const uint32_t k0 = blockIdx.x * KB;
-  if (t < KB) zero[k0 + t] = 0;
-  constexpr uint32_t CPB = KB / SCHED_CHUNK;           // chunks per block
-  uint32_t base = 0;
-  for (uint32_t j = 0; j < blockIdx.x * CPB; ++j) base += total[j];
-  uint32_t mine = 0;
-  for (uint32_t j = 0; j < CPB; ++j) mine += total[blockIdx.x * CPB + j];
-  if (t < KB) {
-    uint32_t cb = base;                                 // base of this bucket's chunk
-    for (uint32_t j = 0; j < t / SCHED_CHUNK; ++j) cb += total[blockIdx.x * CPB + j];
-    loff[t] = cb + start[k0 + t];
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t x = __shfl_up(inc, d);
+    if (lane >= d) inc += x;
   }
-  for (uint32_t i = t; i < mine; i += 1024) perm[base + i] = INF;
-  if (blockIdx.x == SCHED_RANGE_BLOCKS - 1 && t == 0) *nslots = base + mine;
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t all = 0, below = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    below += j < w ? wsum[j] : 0u;
+    all += wsum[j];
+  }
+  if (all > sched_slots_bound(S.C, 64 / CPW)) {          // block-uniform: plain sort fits
+    __syncthreads();
+    tot = plan_chunk<CPW>(cnt, st, false);                                // plain counting sort
+    inc = tot;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(inc, d);
+      if (lane >= d) inc += x;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    all = below = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      below += j < w ? wsum[j] : 0u;
+      all += wsum[j];
+    }
+  }
+  const uint32_t base = below + inc - tot;
+  cbase[t] = base;
+  if (t == SCHED_CHUNKS - 1) cbase[SCHED_CHUNKS] = all;
+  if (blockIdx.x == 0 && t == 0) *nslots = all;
+  constexpr uint32_t CPB = KB / SCHED_CHUNK;            // chunks per block
+  if (t / CPB == blockIdx.x) {                           // this block's chunks: bucket offsets
+#pragma unroll
+    for (uint32_t i = 0; i < SCHED_CHUNK; ++i) loff[(t % CPB) * SCHED_CHUNK + i] = base + st[i];
+  }
+  __syncthreads();
+  const uint32_t s0 = cbase[blockIdx.x * CPB], s1 = cbase[(blockIdx.x + 1) * CPB];
+  for (uint32_t i = s0 + t; i < s1; i += 1024) perm[i] = INF;
   __syncthreads();                      // the empty marks land before the placements
   // keys as 16-byte vectors, sixteen loads in flight per thread (64 keys), then the scalar tail
   const uint32_t C4 = S.C / 4;
@@ -1287,21 +1317,18 @@ hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* plan,
-                             uint32_t* nslots, hipStream_t st) {
-  uint32_t* total = plan + SCHED_BUCKETS;
+hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
+                             hipStream_t st) {
   switch (64 / S.N) {
-#define RS_PLAN(CPW)                                                                           \
-  case CPW:                                                                                    \
-    hipLaunchKernelGGL(sched_plan_kernel<CPW>, dim3(1), dim3(SCHED_CHUNKS), 0, st, S, plan,    \
-                       total);                                                                 \
+#define RS_PLAN(CPW)                                                                             \
+  case CPW:                                                                                      \
+    hipLaunchKernelGGL(sched_range_kernel<CPW>, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S,  \
+                       zero, perm, nslots);                                                      \
     break;
     RS_PLAN(32) RS_PLAN(21) RS_PLAN(16) RS_PLAN(12) RS_PLAN(10) RS_PLAN(9) RS_PLAN(8) RS_PLAN(7)
 #undef RS_PLAN
     default: return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(sched_range_kernel, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, zero,
-                     perm, plan, total, nslots);
   return hipGetLastError();
 }
 
@@ -1392,34 +1419,41 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
   out[ci] = h;
 }
 
+// The tick kernel's own start/stop timestamps go into ev0/ev1 through its dispatch packet
+// (hipExtLaunchKernelGGL): no marker packets between launches (each cost ~5.7 us of idle GPU).
 template <int N, bool SPEC>
-void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
+                    hipEvent_t ev1) {
   constexpr int CPW = 64 / N;
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = S.perm ? sched_slots_bound(S.C, N) / CPW : (S.C + CPW - 1) / CPW;
   if (S.TC)
-    hipLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(waves), dim3(64), lds, st, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(waves), dim3(64), lds, st, ev0, ev1,
+                          0, S, t0, nt);
   else
-    hipLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(waves), dim3(64), lds, st, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(waves), dim3(64), lds, st, ev0, ev1,
+                          0, S, t0, nt);
 }
 
 template <int N>
-hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
-  if (S.variant & RAFT_VARIANT_SPEC) launch_tick_ns<N, true>(S, t0, nt, st);
-  else launch_tick_ns<N, false>(S, t0, nt, st);
+hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
+                         hipEvent_t ev0, hipEvent_t ev1) {
+  if (S.variant & RAFT_VARIANT_SPEC) launch_tick_ns<N, true>(S, t0, nt, st, ev0, ev1);
+  else launch_tick_ns<N, false>(S, t0, nt, st, ev0, ev1);
   return hipGetLastError();
 }
 
-hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st) {
+hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
+                       hipEvent_t ev1) {
   switch (S.N) {
-    case 2: return launch_tick_n<2>(S, t0, nt, st);
-    case 3: return launch_tick_n<3>(S, t0, nt, st);
-    case 4: return launch_tick_n<4>(S, t0, nt, st);
-    case 5: return launch_tick_n<5>(S, t0, nt, st);
-    case 6: return launch_tick_n<6>(S, t0, nt, st);
-    case 7: return launch_tick_n<7>(S, t0, nt, st);
-    case 8: return launch_tick_n<8>(S, t0, nt, st);
-    case 9: return launch_tick_n<9>(S, t0, nt, st);
+    case 2: return launch_tick_n<2>(S, t0, nt, st, ev0, ev1);
+    case 3: return launch_tick_n<3>(S, t0, nt, st, ev0, ev1);
+    case 4: return launch_tick_n<4>(S, t0, nt, st, ev0, ev1);
+    case 5: return launch_tick_n<5>(S, t0, nt, st, ev0, ev1);
+    case 6: return launch_tick_n<6>(S, t0, nt, st, ev0, ev1);
+    case 7: return launch_tick_n<7>(S, t0, nt, st, ev0, ev1);
+    case 8: return launch_tick_n<8>(S, t0, nt, st, ev0, ev1);
+    case 9: return launch_tick_n<9>(S, t0, nt, st, ev0, ev1);
     default: return hipErrorInvalidValue;
   }
 }
