@@ -17,7 +17,7 @@ Per workload:
                 64 B per delivered message (written and read once) and 16 B per appended log entry
                 (read and written once), over the average launch time measured with HIP events on
                 the simulator's stream. `traffic` is the PMC-measured HBM bytes per launch from
-                profiles/pmc_traffic.json, used only when it was measured on this kernel build
+                pmc_traffic.json (scripts/summarize_profile.py), used only when it was measured on this kernel build
                 (source hash match). SURVEY §8(d)'s per-node-tick formula, which charges the skipped
                 idle ticks as if they moved state, is reported as `per_tick_model` (informational).
   cpu_baseline  the C oracle (oracle/raftref.c, the restatement of core.clj/log.clj; "port") on a
@@ -70,7 +70,7 @@ def kernel_build_hash():
 
 def load_traffic(workload):
     """PMC HBM bytes per tick-kernel launch measured on THIS kernel source (else None)."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
+    f = ROOT / "pmc_traffic.json"     # written by scripts/summarize_profile.py
     try:
         rec = json.loads(f.read_text()).get(workload)
     except (OSError, ValueError):

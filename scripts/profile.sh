@@ -23,3 +23,11 @@ for PMC in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 240 rocprofv3 --pmc $PMC --output-format csv -d $OUT/pmc$i -o run -- python3 $B > $OUT/pmc$i.log 2>&1 || { echo "pmc$i failed $?"; exit 1; }
   echo "pmc$i ok"
 done
+# FETCH_SIZE / WRITE_SIZE calibration over known byte counts (scripts/fetch_probe.hip)
+PROBE=/tmp/fetch_probe_$$
+hipcc --offload-arch=gfx950 -O3 -o $PROBE $R/scripts/fetch_probe.hip > $OUT/probe_build.log 2>&1 || { echo "probe build failed"; exit 1; }
+$PROBE > $OUT/probe_spans.txt 2>&1 || { echo "probe failed $?"; exit 1; }
+for PMC in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 60 rocprofv3 --pmc $PMC --output-format csv -d $OUT/cal_$PMC -o run -- $PROBE > $OUT/cal_$PMC.log 2>&1 || { echo "cal $PMC failed $?"; exit 1; }
+  echo "cal $PMC ok"
+done

@@ -1,12 +1,22 @@
-"""Summarize a scripts/profile.sh run (gpurun_out/prof_TAG) into profiles/TAG_*.
+"""Summarize a scripts/profile.sh run (gpurun_out/prof_TAG_WL/) into profiles/ and pmc_traffic.json.
 
-Writes profiles/TAG_kernel_stats.csv (rocprofv3 --stats output, verbatim), profiles/TAG_pmc.json
-(per-launch averages of every PMC counter for the tick kernel) and profiles/pmc_traffic.json
-(HBM bytes per tick-kernel launch for bench.py's roofline.traffic). HBM bytes follow
-MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB from the memory-side request counters;
-on gfx950 FETCH_SIZE reads half the bytes of wide coalesced streaming reads, so both the raw value
-and the x2-corrected read side are recorded (this kernel's reads are narrow gathers, for which the
-guide gives no calibration; the write side dominates here).
+Usage: python scripts/summarize_profile.py TAG WL
+
+Writes
+  profiles/TAG_WL_kernel_stats.csv   rocprofv3 --stats of the bench run, verbatim
+  profiles/TAG_WL_pmc.json           per-launch averages of every PMC counter for the tick kernel,
+                                     the bench line of the profiled run, the FETCH_SIZE/WRITE_SIZE
+                                     calibration and the roofline recomputed from these files alone
+  profiles/TAG_fetch_calibration.json  the probe table (scripts/fetch_probe.hip)
+  pmc_traffic.json                   {WL: {hbm_bytes_per_launch, kernel_src_sha, ...}} which
+                                     bench.py reports as roofline.traffic when the kernel sources
+                                     still hash to kernel_src_sha
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB counted at the memory
+side. Rather than a blanket x2 read correction, each counter is divided by the counter-bytes-per-
+true-byte ratio k that fetch_probe measured for the access shapes the tick kernel issues: its
+reads are node SoA words (4 B per lane, contiguous: k_u32) and 32 B queue slots / 8 B log entries
+(k_msg32), mixed in the proportion the event model assigns them (state vs message+entry bytes).
 """
 import collections
 import csv
@@ -16,30 +26,127 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-src = ROOT / "gpurun_out" / f"prof_{tag}"
-dst = ROOT / "profiles"
-dst.mkdir(exist_ok=True)
-shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
-pmc = collections.defaultdict(list)
-for f in sorted(src.glob("pmc*/run_counter_collection.csv")):
-    for r in csv.DictReader(open(f)):
-        if "tick_kernel" in r["Kernel_Name"]:
-            pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-avg = {k: sum(v) / len(v) for k, v in pmc.items()}
-trace = list(csv.DictReader(open(src / "kt" / "run_kernel_trace.csv")))
-durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
-        if "tick_kernel" in r["Kernel_Name"]]
-fetch, write = avg.get("FETCH_SIZE", 0) * 1024, avg.get("WRITE_SIZE", 0) * 1024
-out = {"tag": tag, "kernel": "rs::tick_kernel<5>", "launches_profiled": len(durs),
-       "avg_duration_ns": sum(durs) / max(1, len(durs)),
-       "vgpr": next((r.get("VGPR_Count") for r in trace if "tick_kernel" in r["Kernel_Name"]), None),
-       "pmc_per_launch": avg,
-       "hbm_fetch_bytes_raw": fetch, "hbm_write_bytes": write,
-       "hbm_bytes_per_launch": 2 * fetch + write,
-       "note": "2*FETCH_SIZE + WRITE_SIZE per the gfx950 FETCH_SIZE correction; see docstring"}
-(dst / f"{tag}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
-(dst / "pmc_traffic.json").write_text(json.dumps(
-    {"source": f"profiles/{tag}_pmc.json", "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
-     "workload": "C2 bench, 10,000 ticks per launch"}, indent=1) + "\n")
-print(json.dumps(out, indent=1))
+KERNEL = "tick_kernel"
+
+
+def counters_by_kernel(path):
+    """{kernel substring match -> {counter: [values per dispatch]}} from a counter_collection csv."""
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(path.glob("**/*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def calibration(src):
+    spans = {}
+    for line in (src / "probe_spans.txt").read_text().splitlines():
+        p = line.split()
+        if len(p) == 4 and p[0] == "probe":
+            spans[p[1]] = (int(p[2]), int(p[3]))
+    table = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        for kname, vals in counters_by_kernel(src / f"cal_{ctr}").items():
+            for probe, (span, req) in spans.items():
+                if probe in kname and ctr in vals and (probe.startswith("rd") == (ctr == "FETCH_SIZE")):
+                    b = sum(vals[ctr]) * 1024
+                    table[probe] = {"counter": ctr, "counter_bytes": b, "span_bytes": span,
+                                    "requested_bytes": req, "k_span": b / span,
+                                    "k_requested": b / req}
+    return table
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r09"
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
+    src = ROOT / "gpurun_out" / f"prof_{tag}_{wl}"
+    dst = ROOT / "profiles"
+    dst.mkdir(exist_ok=True)
+    shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_{wl}_kernel_stats.csv")
+
+    bench = next(json.loads(l) for l in (src / "kt.log").read_text().splitlines()
+                 if l.startswith('{"metric"'))
+    pmc = collections.defaultdict(list)
+    for i in range(1, 20):
+        d = src / f"pmc{i}"
+        if not d.exists():
+            continue
+        for kname, vals in counters_by_kernel(d).items():
+            if KERNEL in kname:
+                for c, v in vals.items():
+                    pmc[c].extend(v)
+    avg = {k: sum(v) / len(v) for k, v in pmc.items()}
+    trace = list(csv.DictReader(open(src / "kt" / "run_kernel_trace.csv")))
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
+            if KERNEL in r["Kernel_Name"]]
+    stats = [r for r in csv.DictReader(open(src / "kt" / "run_kernel_stats.csv"))
+             if KERNEL in r["Name"]]
+    durs = durs[-max(1, bench["roofline"]["launches"]):]   # the timed launches, not the warm-up
+    avg_ns = sum(durs) / max(1, len(durs))
+
+    cal = calibration(src)
+    (dst / f"{tag}_fetch_calibration.json").write_text(json.dumps(cal, indent=1) + "\n")
+    roof = bench["roofline"]
+    cnt = bench["counters"]
+    n = bench["config"]["nodes"]
+    nodes = bench["config"]["clusters_per_gpu"] * n
+    launches = max(1, roof["launches"])
+    state_rd = (32 + 8 * n) * nodes
+    msg_rd = (32 * cnt.get("delivered", 0) + 8 * cnt.get("entries_appended", 0)) / launches
+    w_state = state_rd / max(1.0, state_rd + msg_rd)
+    k_rd = w_state * cal["rd_u32_contig"]["k_span"] + (1 - w_state) * cal["rd_msg32_contig"]["k_span"]
+    k_wr = w_state * cal["wr_u32_contig"]["k_span"] + (1 - w_state) * cal["wr_msg32_contig"]["k_span"]
+    fetch_raw, write_raw = avg.get("FETCH_SIZE", 0) * 1024, avg.get("WRITE_SIZE", 0) * 1024
+    hbm = fetch_raw / k_rd + write_raw / k_wr
+    event_bytes = roof["bytes_per_launch"]
+    achieved = event_bytes / (avg_ns * 1e-9) / 1e9
+    out = {
+        "tag": tag, "workload": wl, "kernel_src_sha": roof["kernel_src_sha"],
+        "kernel": next((r["Kernel_Name"] for r in trace if KERNEL in r["Kernel_Name"]), None),
+        "launches_traced": len(durs), "avg_duration_ns_trace": avg_ns,
+        "avg_duration_ns_stats": float(stats[0]["AverageNs"]) if stats else None,
+        "bench_avg_launch_ms_hip_events": roof["avg_launch_ms"],
+        "vgpr": next((r.get("VGPR_Count") for r in trace if KERNEL in r["Kernel_Name"]), None),
+        "pmc_per_launch": avg,
+        # occupancy and clock (MI355X_MICROARCH.md: SQ_WAVE_CYCLES in quad-cycles summed over
+        # waves; GRBM_GUI_ACTIVE summed over the 8 XCDs): mean resident waves per CU over the
+        # launch, and the effective shader clock
+        "derived": {
+            "mean_waves_per_cu": 4 * avg["SQ_WAVE_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 256)
+            if avg.get("GRBM_GUI_ACTIVE") and "SQ_WAVE_CYCLES" in avg else None,
+            "effective_clock_GHz": avg["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+            if avg.get("GRBM_GUI_ACTIVE") else None,
+            "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+            if avg.get("SQ_WAVES") and "SQ_INSTS_VALU" in avg else None},
+        "calibration": {"k_read": k_rd, "k_write": k_wr, "state_read_weight": w_state,
+                        "source": f"profiles/{tag}_fetch_calibration.json"},
+        "hbm_fetch_bytes_raw": fetch_raw, "hbm_write_bytes_raw": write_raw,
+        "hbm_bytes_per_launch": hbm,
+        "roofline_recomputed": {
+            "event_bytes_per_launch": event_bytes,
+            "event_bytes_terms": {"state_in_out": 2 * (32 + 8 * n) * nodes,
+                                  "messages_64B": 64 * cnt.get("delivered", 0) / launches,
+                                  "entries_16B": 16 * cnt.get("entries_appended", 0) / launches},
+            "achieved_GBs": achieved, "peak_GBs": 8000.0, "frac": achieved / 8000.0,
+            "traffic_over_event_bytes": hbm / event_bytes if event_bytes else None,
+            "how": "event_bytes_per_launch / avg_duration_ns_trace; event bytes from the bench "
+                   "line's counters (bench_line below)"},
+        "bench_line": bench,
+    }
+    (dst / f"{tag}_{wl}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
+    tf = ROOT / "pmc_traffic.json"
+    try:
+        traffic = json.loads(tf.read_text())
+    except (OSError, ValueError):
+        traffic = {}
+    traffic[wl] = {"hbm_bytes_per_launch": hbm, "kernel_src_sha": roof["kernel_src_sha"],
+                   "source": f"profiles/{tag}_{wl}_pmc.json"}
+    tf.write_text(json.dumps(traffic, indent=1, sort_keys=True) + "\n")
+    print(json.dumps({k: out[k] for k in ("workload", "avg_duration_ns_trace",
+                                          "bench_avg_launch_ms_hip_events", "calibration",
+                                          "hbm_bytes_per_launch", "roofline_recomputed")},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
