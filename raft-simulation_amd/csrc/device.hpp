@@ -1,13 +1,18 @@
 // device.hpp — device-side building blocks of the tick kernel (gfx950 / CDNA4).
 //
-// Layout in HBM (structure of arrays, node index gi = cluster * N + k, k = id - 1):
-//   hot node words   flags, masks, term, commit, len, deadline, qmeta, req/res head+tail arrival,
-//                    arena base/frontier, last_led, trace lo/hi           [NN] u32 each
-//   cold node words  next_index / match_index                              [N][NN] i32
+// Layout in HBM (node index gi = cluster * N + k, k = id - 1):
+//   hot state        hot[c][HB]: one 128-B-aligned block per cluster holding every per-node word
+//                    the tick kernel loads at launch start and stores at its end, field-major
+//                    inside the block (word f * N + k = field f of node k; fields HotField below,
+//                    next_index / match_index as N fields each), then the cluster's 8 words
+//                    (raft_cluster_t: hwm index, term, val, client_next, client_count, 0, 0, 0).
+//                    A wave's clusters come from the packing permutation, i.e. from anywhere in
+//                    the shard: a block per cluster makes the wave's state load touch only its own
+//                    clusters' lines (the structure-of-arrays layout read ~13 lines per load)
 //   queues           qbuf[which][slot][gi] of 8-word messages (ring per node, sorted by arrival);
 //                    slot-major so the same ring slot of a cluster's nodes is contiguous
 //   log arenas       arena[gi][A] of (term, val)
-//   cluster words    cl[c] = raft_cluster_t (hwm index, term, val, client_next, client_count, 0,0,0)
+//   cold node words  ccount (commit_count), commit-stream / trace rings               [NN]...
 // A wave owns floor(64 / N) whole clusters, one lane per node; a cluster never spans waves, so all
 // intra-cluster traffic is lane-to-lane inside one wave (LDS cells + ds_bpermute).
 #pragma once
@@ -35,12 +40,10 @@ struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
   uint32_t hb, el_base, el_span, drop_ppm, dup_ppm, dmin, dmax, part_ppm, part_epoch,
       client_ppm, variant, client_period, client_burst, client_redirects;
-  uint32_t *flags, *masks, *term, *commit, *len, *deadline, *qmeta, *req_arr, *res_arr,
-      *req_tail, *res_tail, *abase, *afront, *led, *trace_lo, *trace_hi;
-  int32_t *next, *match;  // [N][NN], row p-1 for peer id p
+  uint32_t* hot;          // [C][HB] cluster blocks (HotField, hot_cl_off, hot_block_words)
+  uint32_t HB;            // hot_block_words(N)
   uint32_t* qbuf;         // [2][Q][NN][8]
   uint32_t* arena;        // [NN][A][2]
-  uint32_t* cl;           // [C][8] raft_cluster_t
   uint32_t* ccount;       // [NN] commit_count (F2)
   uint32_t* stream;       // [NN][SC] commit-stream rings (F2)
   uint32_t SC;            // commit_stream_cap
@@ -58,6 +61,26 @@ struct DevSim {
   uint32_t* shist;          // [SCHED_BUCKETS] histogram of skey (null: schedule fixed)
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
 };
+
+// Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
+// id p is field HF_NEXT + p - 1, match_index field HF_NEXT + N + p - 1; the cluster's 8 words
+// start at hot_cl_off(N). Blocks are whole 128-B lines.
+enum HotField : uint32_t {
+  HF_FLAGS, HF_MASKS, HF_TERM, HF_COMMIT, HF_LEN, HF_DEADLINE, HF_QMETA, HF_REQ_ARR, HF_RES_ARR,
+  HF_REQ_TAIL, HF_RES_TAIL, HF_ABASE, HF_AFRONT, HF_LED, HF_TRACE_LO, HF_TRACE_HI, HF_NEXT
+};
+__host__ __device__ constexpr uint32_t hot_cl_off(uint32_t N) { return (HF_NEXT + 2 * N) * N; }
+__host__ __device__ constexpr uint32_t hot_block_words(uint32_t N) {
+  return (hot_cl_off(N) + 8 + 31) & ~31u;
+}
+// Word 0 of node k's fields in cluster c's block (field f at [f * N]) / the cluster's 8 words.
+__device__ __forceinline__ uint32_t* hot_node(const DevSim& S, uint32_t c, uint32_t k) {
+  return S.hot + (size_t)c * S.HB + k;
+}
+__device__ __forceinline__ uint32_t* hot_cl(const DevSim& S, uint32_t c) {
+  return S.hot + (size_t)c * S.HB + hot_cl_off(S.N);
+}
+
 constexpr uint32_t SCHED_BUCKETS = 16384;   // keys clamp to SCHED_BUCKETS - 1
 constexpr uint32_t SCHED_PAST = 16;         // bucket of "now": keys keep 16 ticks of past
 

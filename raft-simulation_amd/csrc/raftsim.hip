@@ -162,14 +162,10 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   for (int i = 0; i < 32; ++i)
     if (pw[i]) d.client_top = i;
   const size_t NN = s->NN;
-  uint32_t** hot[] = {&d.flags, &d.masks, &d.term, &d.commit, &d.len, &d.deadline, &d.qmeta,
-                      &d.req_arr, &d.res_arr, &d.req_tail, &d.res_tail, &d.abase, &d.afront,
-                      &d.led, &d.trace_lo, &d.trace_hi};
-  for (uint32_t** p : hot)
-    if ((rc = dalloc(s, p, NN))) { sh_destroy(s); return rc; }
-  if ((rc = dalloc(s, &d.next, NN * s->N)) || (rc = dalloc(s, &d.match, NN * s->N)) ||
+  d.HB = rs::hot_block_words(s->N);
+  if ((rc = dalloc(s, &d.hot, (size_t)s->C * d.HB)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
-      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) || (rc = dalloc(s, &d.cl, (size_t)s->C * 8)) ||
+      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) ||
       (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 2)) || (rc = dalloc(s, &s->client_pw, 32)) ||
       (rc = dalloc(s, &d.ccount, NN)) ||
       (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1))) ||
@@ -201,8 +197,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreate(&s->ev_start)) != hipSuccess ||
       (e = hipEventCreate(&s->ev_stop)) != hipSuccess ||
-      (e = hipMemsetAsync(d.next, 0, NN * s->N * 4, s->stream)) != hipSuccess ||
-      (e = hipMemsetAsync(d.match, 0, NN * s->N * 4, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.hot, 0, (size_t)s->C * d.HB * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
@@ -306,6 +301,14 @@ static uint32_t* qring(Shard* s, uint32_t gi, uint32_t which) {
   return s->d.qbuf + ((size_t)which * s->Q * s->NN + gi) * 8;
 }
 
+// Field `f` of node `id` in cluster `cluster`'s hot block (rs::HotField).
+static uint32_t* hot_word(Shard* s, uint32_t cluster, uint32_t id, uint32_t f) {
+  return s->d.hot + (size_t)cluster * s->d.HB + (size_t)f * s->N + (id - 1);
+}
+static uint32_t* cl_words(Shard* s, uint32_t cluster) {
+  return s->d.hot + (size_t)cluster * s->d.HB + rs::hot_cl_off(s->N);
+}
+
 static int check_node(Shard* s, uint32_t cluster, uint32_t id) {
   if (!s) return fail(-EINVAL, "null sim");
   if (cluster >= s->C || id < 1 || id > s->N) return fail(-EINVAL, "cluster/node out of bounds");
@@ -326,37 +329,31 @@ static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
   if (rc) return rc;
   if (!out) return fail(-EINVAL, "null output");
   HIP_OK(hipSetDevice(s->cfg.device));
-  const size_t n0 = (size_t)c0 * s->N, cnt = (size_t)nc * s->N, NN = s->NN, N = s->N;
-  std::vector<uint32_t> w(17 * cnt);
-  std::vector<int32_t> nx(N * cnt), mt(N * cnt);
-  const DevSim& d = s->d;
-  const uint32_t* src[17] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.qmeta,
-                             d.req_arr, d.res_arr, d.req_tail, d.res_tail, d.abase, d.afront,
-                             d.led, d.trace_lo, d.trace_hi, d.ccount};
-  for (int f = 0; f < 17; ++f) HIP_OK(d2h(s, &w[f * cnt], src[f] + n0, cnt));
-  for (size_t p = 0; p < N; ++p) {
-    HIP_OK(d2h(s, &nx[p * cnt], d.next + p * NN + n0, cnt));
-    HIP_OK(d2h(s, &mt[p * cnt], d.match + p * NN + n0, cnt));
-  }
+  const size_t n0 = (size_t)c0 * s->N, cnt = (size_t)nc * s->N, N = s->N, HB = s->d.HB;
+  std::vector<uint32_t> blk(nc * HB), cc(cnt);
+  HIP_OK(d2h(s, blk.data(), s->d.hot + (size_t)c0 * HB, nc * HB));
+  HIP_OK(d2h(s, cc.data(), s->d.ccount + n0, cnt));
   HIP_OK(hipStreamSynchronize(s->stream));
   for (size_t i = 0; i < cnt; ++i) {
+    const uint32_t* h = &blk[(i / N) * HB + i % N];     // field f at h[f * N]
+    auto f = [&](uint32_t fld) { return h[fld * N]; };
     raft_node_t& r = out[i];
     memset(&r, 0, sizeof r);
-    const uint32_t fl = w[i], mk = w[cnt + i], qm = w[6 * cnt + i];
+    const uint32_t fl = f(rs::HF_FLAGS), mk = f(rs::HF_MASKS), qm = f(rs::HF_QMETA);
     r.role = fl & 3; r.voted_for = (fl >> 2) & 15; r.leader_id = (fl >> 6) & 15;
     r.fault = (fl >> 10) & 7; r.entries_is_seq = (fl >> 13) & 1; r.ls_present = (fl >> 14) & 1;
     r.votes = mk & 0xFFFF; r.ls_keys = mk >> 16;
-    r.current_term = w[2 * cnt + i]; r.commit_index = w[3 * cnt + i];
-    r.log_len = w[4 * cnt + i]; r.deadline = w[5 * cnt + i];
+    r.current_term = f(rs::HF_TERM); r.commit_index = f(rs::HF_COMMIT);
+    r.log_len = f(rs::HF_LEN); r.deadline = f(rs::HF_DEADLINE);
     for (size_t p = 0; p < N; ++p) {
-      r.next_index[p] = nx[p * cnt + i];
-      r.match_index[p] = mt[p * cnt + i];
+      r.next_index[p] = (int32_t)f(rs::HF_NEXT + p);
+      r.match_index[p] = (int32_t)f(rs::HF_NEXT + N + p);
     }
-    r.last_led_term = w[13 * cnt + i];
-    r.arena_base = w[11 * cnt + i]; r.arena_frontier = w[12 * cnt + i];
+    r.last_led_term = f(rs::HF_LED);
+    r.arena_base = f(rs::HF_ABASE); r.arena_frontier = f(rs::HF_AFRONT);
     r.req_count = (qm >> 4) & 31; r.res_count = (qm >> 13) & 31;
-    r.trace_hash = (uint64_t)w[15 * cnt + i] << 32 | w[14 * cnt + i];
-    r.commit_count = w[16 * cnt + i];
+    r.trace_hash = (uint64_t)f(rs::HF_TRACE_HI) << 32 | f(rs::HF_TRACE_LO);
+    r.commit_count = cc[i];
   }
   return 0;
 }
@@ -367,7 +364,7 @@ static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t*
   if (!in) return fail(-EINVAL, "null input");
   HIP_OK(hipSetDevice(s->cfg.device));
   const uint32_t N = s->N, all = ((1u << (N + 1)) - 1) & ~1u;
-  const size_t n0 = (size_t)c0 * N, cnt = (size_t)nc * N, NN = s->NN;
+  const size_t n0 = (size_t)c0 * N, cnt = (size_t)nc * N;
   for (size_t i = 0; i < cnt; ++i) {
     const raft_node_t* n = &in[i];
     uint32_t id = (uint32_t)(i % N) + 1, peers = all & ~(1u << id);
@@ -380,34 +377,31 @@ static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t*
         (!n->ls_present && n->ls_keys))
       return fail(-EINVAL, "invalid node record");
   }
-  std::vector<uint32_t> w(14 * cnt);
-  std::vector<uint32_t> ccv(cnt);
-  std::vector<int32_t> nx(N * cnt), mt(N * cnt);
+  // the queue words of the blocks (qmeta, head/tail arrivals) and the cluster words are kept
+  const size_t HB = s->d.HB;
+  std::vector<uint32_t> blk(nc * HB), ccv(cnt);
+  HIP_OK(d2h(s, blk.data(), s->d.hot + (size_t)c0 * HB, nc * HB));
+  HIP_OK(hipStreamSynchronize(s->stream));
   for (size_t i = 0; i < cnt; ++i) {
     const raft_node_t& r = in[i];
-    w[i] = rs::pack_flags(r.role, r.voted_for, r.leader_id, r.fault, r.entries_is_seq,
-                          r.ls_present);
-    w[cnt + i] = r.votes | (uint32_t)r.ls_keys << 16;
-    w[2 * cnt + i] = r.current_term; w[3 * cnt + i] = r.commit_index;
-    w[4 * cnt + i] = r.log_len; w[5 * cnt + i] = r.deadline;
-    w[6 * cnt + i] = r.arena_base; w[7 * cnt + i] = r.arena_frontier;
-    w[8 * cnt + i] = r.last_led_term;
-    w[9 * cnt + i] = (uint32_t)r.trace_hash; w[10 * cnt + i] = (uint32_t)(r.trace_hash >> 32);
+    uint32_t* h = &blk[(i / N) * HB + i % N];
+    auto f = [&](uint32_t fld) -> uint32_t& { return h[fld * N]; };
+    f(rs::HF_FLAGS) = rs::pack_flags(r.role, r.voted_for, r.leader_id, r.fault, r.entries_is_seq,
+                                     r.ls_present);
+    f(rs::HF_MASKS) = r.votes | (uint32_t)r.ls_keys << 16;
+    f(rs::HF_TERM) = r.current_term; f(rs::HF_COMMIT) = r.commit_index;
+    f(rs::HF_LEN) = r.log_len; f(rs::HF_DEADLINE) = r.deadline;
+    f(rs::HF_ABASE) = r.arena_base; f(rs::HF_AFRONT) = r.arena_frontier;
+    f(rs::HF_LED) = r.last_led_term;
+    f(rs::HF_TRACE_LO) = (uint32_t)r.trace_hash; f(rs::HF_TRACE_HI) = (uint32_t)(r.trace_hash >> 32);
     ccv[i] = r.commit_count;
     for (size_t p = 0; p < N; ++p) {
-      nx[p * cnt + i] = r.next_index[p];
-      mt[p * cnt + i] = r.match_index[p];
+      f(rs::HF_NEXT + p) = (uint32_t)r.next_index[p];
+      f(rs::HF_NEXT + N + p) = (uint32_t)r.match_index[p];
     }
   }
-  const DevSim& d = s->d;
-  uint32_t* dst[11] = {d.flags, d.masks, d.term, d.commit, d.len, d.deadline, d.abase,
-                       d.afront, d.led, d.trace_lo, d.trace_hi};
-  for (int f = 0; f < 11; ++f) HIP_OK(h2d(s, dst[f] + n0, &w[f * cnt], cnt));
-  HIP_OK(h2d(s, d.ccount + n0, ccv.data(), cnt));
-  for (size_t p = 0; p < N; ++p) {
-    HIP_OK(h2d(s, d.next + p * NN + n0, &nx[p * cnt], cnt));
-    HIP_OK(h2d(s, d.match + p * NN + n0, &mt[p * cnt], cnt));
-  }
+  HIP_OK(h2d(s, s->d.hot + (size_t)c0 * HB, blk.data(), nc * HB));
+  HIP_OK(h2d(s, s->d.ccount + n0, ccv.data(), cnt));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -421,7 +415,7 @@ static int sh_read_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which
   const uint32_t gi = cluster * s->N + id - 1;
   uint32_t qm = 0;
   std::vector<raft_msg_t> slots(s->Q);
-  HIP_OK(d2h(s, &qm, s->d.qmeta + gi, 1));
+  HIP_OK(d2h(s, &qm, hot_word(s, cluster, id, rs::HF_QMETA), 1));
   HIP_OK(hipMemcpy2DAsync(slots.data(), sizeof(raft_msg_t), qring(s, gi, which),
                           (size_t)s->NN * sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q,
                           hipMemcpyDeviceToHost, s->stream));
@@ -451,7 +445,7 @@ static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t whic
   memset(slots.data(), 0, s->Q * sizeof(raft_msg_t));
   for (uint32_t i = 0; i < count; ++i) slots[i] = in[i];
   uint32_t qm = 0;
-  HIP_OK(d2h(s, &qm, s->d.qmeta + gi, 1));
+  HIP_OK(d2h(s, &qm, hot_word(s, cluster, id, rs::HF_QMETA), 1));
   HIP_OK(hipStreamSynchronize(s->stream));
   if (which) qm = (qm & ~(0xFu << 9 | 0x1Fu << 13)) | count << 13;
   else qm = (qm & ~0x1FFu) | count << 4;
@@ -459,9 +453,9 @@ static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t whic
   HIP_OK(hipMemcpy2DAsync(qring(s, gi, which), (size_t)s->NN * sizeof(raft_msg_t), slots.data(),
                           sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q, hipMemcpyHostToDevice,
                           s->stream));
-  HIP_OK(h2d(s, s->d.qmeta + gi, &qm, 1));
-  HIP_OK(h2d(s, (which ? s->d.res_arr : s->d.req_arr) + gi, &harr, 1));
-  HIP_OK(h2d(s, (which ? s->d.res_tail : s->d.req_tail) + gi, &tail, 1));
+  HIP_OK(h2d(s, hot_word(s, cluster, id, rs::HF_QMETA), &qm, 1));
+  HIP_OK(h2d(s, hot_word(s, cluster, id, which ? rs::HF_RES_ARR : rs::HF_REQ_ARR), &harr, 1));
+  HIP_OK(h2d(s, hot_word(s, cluster, id, which ? rs::HF_RES_TAIL : rs::HF_REQ_TAIL), &tail, 1));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -585,8 +579,9 @@ static int sh_read_clusters(Shard* s, uint32_t c0, uint32_t nc, raft_cluster_t* 
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
   static_assert(sizeof(raft_cluster_t) == 32, "cluster record is 8 words");
-  HIP_OK(hipMemcpyAsync(out, s->d.cl + (size_t)c0 * 8, nc * sizeof(raft_cluster_t),
-                        hipMemcpyDeviceToHost, s->stream));
+  if (nc)    // the cluster words sit at a fixed offset of each block
+    HIP_OK(hipMemcpy2DAsync(out, sizeof(raft_cluster_t), cl_words(s, c0), (size_t)s->d.HB * 4,
+                            sizeof(raft_cluster_t), nc, hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -597,8 +592,10 @@ static int sh_write_clusters(Shard* s, uint32_t c0, uint32_t nc, const raft_clus
   HIP_OK(hipSetDevice(s->cfg.device));
   std::vector<raft_cluster_t> buf(in, in + nc);
   for (auto& h : buf) h.reserved[0] = h.reserved[1] = h.reserved[2] = 0;
-  HIP_OK(hipMemcpyAsync(s->d.cl + (size_t)c0 * 8, buf.data(), nc * sizeof(raft_cluster_t),
-                        hipMemcpyHostToDevice, s->stream));
+  if (nc)
+    HIP_OK(hipMemcpy2DAsync(cl_words(s, c0), (size_t)s->d.HB * 4, buf.data(),
+                            sizeof(raft_cluster_t), sizeof(raft_cluster_t), nc,
+                            hipMemcpyHostToDevice, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }

@@ -76,9 +76,9 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
   sentmask |= 1u << p;
 }
 
-// A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are
-// [N][NN] (row per peer); kernels with a small N keep the wave's rows in LDS for the whole launch
-// (NM_LDS below) so heartbeats and append-responses pay no global round trip for them.
+// A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are fields
+// of the cluster block (stride N); kernels with a small N keep the wave's rows in LDS for the whole
+// launch (NM_LDS below) so heartbeats and append-responses pay no global round trip for them.
 struct PeerW {
   int32_t* nx;
   int32_t* mt;
@@ -406,29 +406,33 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   const uint32_t gi = c * N + k0;
   const uint32_t g = S.goff + c;
   const int bl0 = (cs < CPW ? cs : 0) * N;     // the cluster's first lane
-  const uint32_t NN = S.NN, A = S.A;
+  const uint32_t A = S.A;
+  constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
+  // this node's words in its cluster's block (field f at hp[f * N]) and the cluster's words
+  uint32_t* const hp = S.hot + (size_t)c * HB + k0;
+  uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
 
   NodeR n = {};
   uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
   uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
   if (active) {
-    const uint32_t fl = S.flags[gi], mk = S.masks[gi], qm = S.qmeta[gi];
+    const uint32_t fl = hp[HF_FLAGS * N], mk = hp[HF_MASKS * N], qm = hp[HF_QMETA * N];
     n.role = fl & 3; n.vf = (fl >> 2) & 15; n.lid = (fl >> 6) & 15; n.fault = (fl >> 10) & 7;
     n.seq = (fl >> 13) & 1; n.lsp = (fl >> 14) & 1;
     n.votes = mk & 0xFFFF; n.keys = mk >> 16;
-    n.term = S.term[gi]; n.commit = S.commit[gi]; n.len = S.len[gi]; n.deadline = S.deadline[gi];
+    n.term = hp[HF_TERM * N]; n.commit = hp[HF_COMMIT * N]; n.len = hp[HF_LEN * N];
+    n.deadline = hp[HF_DEADLINE * N];
     n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
-    n.rq.arr = S.req_arr[gi]; n.rs.arr = S.res_arr[gi];
-    n.rq.tail = S.req_tail[gi]; n.rs.tail = S.res_tail[gi];
-    n.base = S.abase[gi]; n.front = S.afront[gi]; n.led = S.led[gi];
-    n.trace = (uint64_t)S.trace_hi[gi] << 32 | S.trace_lo[gi];
-    hidx = S.cl[c * 8]; hterm = S.cl[c * 8 + 1]; hval = S.cl[c * 8 + 2];
-    cnext = S.cl[c * 8 + 3]; ccount = S.cl[c * 8 + 4];
+    n.rq.arr = hp[HF_REQ_ARR * N]; n.rs.arr = hp[HF_RES_ARR * N];
+    n.rq.tail = hp[HF_REQ_TAIL * N]; n.rs.tail = hp[HF_RES_TAIL * N];
+    n.base = hp[HF_ABASE * N]; n.front = hp[HF_AFRONT * N]; n.led = hp[HF_LED * N];
+    n.trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
+    hidx = hc[0]; hterm = hc[1]; hval = hc[2]; cnext = hc[3]; ccount = hc[4];
     if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
 #pragma unroll
       for (int p = 0; p < N; ++p) {
-        nmL[p * 64 + lane] = S.next[p * NN + gi];
-        nmL[(N + p) * 64 + lane] = S.match[p * NN + gi];
+        nmL[p * 64 + lane] = hp[(HF_NEXT + p) * N];
+        nmL[(N + p) * 64 + lane] = hp[(HF_NEXT + N + p) * N];
       }
     }
   }
@@ -473,8 +477,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t* const mycells = cells + bl * (N - 1) * CELLW;
     uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
     uint2* const sar = arena_of(S, sgi);
+    int32_t* const hnm = reinterpret_cast<int32_t*>(S.hot + (size_t)(sg - S.goff) * HB + k);
     const PeerW lsw = nm_lds<N>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
-                                 : PeerW{S.next + sgi, S.match + sgi, NN};
+                                 : PeerW{hnm + HF_NEXT * N, hnm + (HF_NEXT + N) * N, (uint32_t)N};
     if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
       fr[lane] = n.front;
       __builtin_amdgcn_wave_barrier();
@@ -1120,24 +1125,24 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
   if (active) {
-    S.flags[gi] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
-    S.masks[gi] = n.votes | n.keys << 16;
-    S.term[gi] = n.term; S.commit[gi] = n.commit; S.len[gi] = n.len; S.deadline[gi] = n.deadline;
-    S.qmeta[gi] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
-    S.req_arr[gi] = n.rq.arr; S.res_arr[gi] = n.rs.arr;
-    S.req_tail[gi] = n.rq.tail; S.res_tail[gi] = n.rs.tail;
-    S.abase[gi] = n.base; S.afront[gi] = n.front; S.led[gi] = n.led;
-    S.trace_lo[gi] = (uint32_t)n.trace; S.trace_hi[gi] = (uint32_t)(n.trace >> 32);
+    hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
+    hp[HF_MASKS * N] = n.votes | n.keys << 16;
+    hp[HF_TERM * N] = n.term; hp[HF_COMMIT * N] = n.commit; hp[HF_LEN * N] = n.len;
+    hp[HF_DEADLINE * N] = n.deadline;
+    hp[HF_QMETA * N] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
+    hp[HF_REQ_ARR * N] = n.rq.arr; hp[HF_RES_ARR * N] = n.rs.arr;
+    hp[HF_REQ_TAIL * N] = n.rq.tail; hp[HF_RES_TAIL * N] = n.rs.tail;
+    hp[HF_ABASE * N] = n.base; hp[HF_AFRONT * N] = n.front; hp[HF_LED * N] = n.led;
+    hp[HF_TRACE_LO * N] = (uint32_t)n.trace; hp[HF_TRACE_HI * N] = (uint32_t)(n.trace >> 32);
     if constexpr (nm_lds<N>()) {
 #pragma unroll
       for (int p = 0; p < N; ++p) {
-        S.next[p * NN + gi] = nmL[p * 64 + lane];
-        S.match[p * NN + gi] = nmL[(N + p) * 64 + lane];
+        hp[(HF_NEXT + p) * N] = nmL[p * 64 + lane];
+        hp[(HF_NEXT + N + p) * N] = nmL[(N + p) * 64 + lane];
       }
     }
     if (k0 == 0) {
-      S.cl[c * 8] = hidx; S.cl[c * 8 + 1] = hterm; S.cl[c * 8 + 2] = hval;
-      S.cl[c * 8 + 3] = cnext; S.cl[c * 8 + 4] = ccount;
+      hc[0] = hidx; hc[1] = hterm; hc[2] = hval; hc[3] = cnext; hc[4] = ccount;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -1165,13 +1170,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= S.C) return;
-  uint32_t m = S.cl[c * 8 + 3];
+  uint32_t m = hot_cl(S, c)[3];
   for (uint32_t k = 0; k < S.N; ++k) {
-    const uint32_t gi = c * S.N + k;
-    if ((S.flags[gi] >> 10) & 7) continue;
-    const uint32_t qm = S.qmeta[gi];
-    const QueueR rq = {0, (qm >> 4) & 31, S.req_arr[gi], 0}, rs = {0, (qm >> 13) & 31, S.res_arr[gi], 0};
-    m = min(m, sched_key_of(S.deadline[gi], rq, rs));
+    const uint32_t* h = hot_node(S, c, k);
+    if ((h[HF_FLAGS * S.N] >> 10) & 7) continue;
+    const uint32_t qm = h[HF_QMETA * S.N];
+    const QueueR rq = {0, (qm >> 4) & 31, h[HF_REQ_ARR * S.N], 0},
+                 rs = {0, (qm >> 13) & 31, h[HF_RES_ARR * S.N], 0};
+    m = min(m, sched_key_of(h[HF_DEADLINE * S.N], rq, rs));
   }
   const uint32_t key = sched_bucket(m, t0);
   S.skey[c] = key;
@@ -1338,11 +1344,14 @@ __global__ void init_kernel(DevSim S) {
   if (gi >= S.NN) return;
   const uint32_t c = gi / S.N, id = gi - c * S.N + 1;
   const uint4 w = philox(S.goff + c, id | P_INIT << 8, 0, 0, S.key0, S.key1);
-  S.flags[gi] = 0; S.masks[gi] = 0; S.term[gi] = 1; S.commit[gi] = 0; S.len[gi] = 0;
-  S.deadline[gi] = S.el_base + __umulhi(w.y, S.el_span);
-  S.qmeta[gi] = 0; S.req_arr[gi] = INF; S.res_arr[gi] = INF; S.req_tail[gi] = 0;
-  S.res_tail[gi] = 0; S.abase[gi] = 0; S.afront[gi] = 0; S.led[gi] = 0; S.ccount[gi] = 0;
-  S.trace_lo[gi] = 0x84222325u; S.trace_hi[gi] = 0xCBF29CE4u;
+  uint32_t* h = hot_node(S, c, id - 1);
+  const uint32_t N = S.N;
+  for (uint32_t f = 0; f < HF_NEXT + 2 * N; ++f) h[f * N] = 0;    // incl. next / match
+  h[HF_TERM * N] = 1;
+  h[HF_DEADLINE * N] = S.el_base + __umulhi(w.y, S.el_span);
+  h[HF_REQ_ARR * N] = INF; h[HF_RES_ARR * N] = INF;
+  h[HF_TRACE_LO * N] = 0x84222325u; h[HF_TRACE_HI * N] = 0xCBF29CE4u;
+  S.ccount[gi] = 0;
   if (id == 1) {                                   // cluster record: no hwm, first client-set
     uint32_t first = INF;
     if (S.client_ppm) {
@@ -1350,8 +1359,9 @@ __global__ void init_kernel(DevSim S) {
       first = on_tick(client_gap(d.x, S.client_pw, S.client_top), S.client_period,
                       S.client_burst);
     }
-    for (int i = 0; i < 8; ++i) S.cl[c * 8 + i] = 0;
-    S.cl[c * 8 + 3] = first;
+    uint32_t* cw = hot_cl(S, c);
+    for (int i = 0; i < 8; ++i) cw[i] = 0;
+    cw[3] = first;
   }
 }
 
@@ -1359,22 +1369,23 @@ __global__ void init_kernel(DevSim S) {
 __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long long* out) {
   const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nc) return;
-  const uint32_t c = c0 + ci, N = S.N, NN = S.NN;
+  const uint32_t c = c0 + ci, N = S.N;
   uint64_t h = 0xCBF29CE484222325ull;
   for (uint32_t k = 0; k < N; ++k) {
     const uint32_t gi = c * N + k;
-    const uint32_t fl = S.flags[gi], mk = S.masks[gi], qm = S.qmeta[gi];
+    const uint32_t* hw = hot_node(S, c, k);
+    const uint32_t fl = hw[HF_FLAGS * N], mk = hw[HF_MASKS * N], qm = hw[HF_QMETA * N];
     const uint32_t w[12] = {fl & 3, (fl >> 2) & 15, (fl >> 6) & 15, (fl >> 10) & 7,
-                            (fl >> 13) & 1, (fl >> 14) & 1, mk & 0xFFFF, mk >> 16, S.term[gi],
-                            S.commit[gi], S.len[gi], S.deadline[gi]};
+                            (fl >> 13) & 1, (fl >> 14) & 1, mk & 0xFFFF, mk >> 16,
+                            hw[HF_TERM * N], hw[HF_COMMIT * N], hw[HF_LEN * N],
+                            hw[HF_DEADLINE * N]};
     for (int i = 0; i < 12; ++i) h = fnv(h, w[i]);
-    for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)S.next[p * NN + gi]);
-    for (uint32_t p = 0; p < N; ++p) h = fnv(h, (uint32_t)S.match[p * NN + gi]);
-    h = fnv(h, S.led[gi]);
-    h = fnv(h, S.trace_lo[gi]);
-    h = fnv(h, S.trace_hi[gi]);
-    h = fnv(h, S.abase[gi]);
-    h = fnv(h, S.afront[gi]);
+    for (uint32_t p = 0; p < 2 * N; ++p) h = fnv(h, hw[(HF_NEXT + p) * N]);   // next, then match
+    h = fnv(h, hw[HF_LED * N]);
+    h = fnv(h, hw[HF_TRACE_LO * N]);
+    h = fnv(h, hw[HF_TRACE_HI * N]);
+    h = fnv(h, hw[HF_ABASE * N]);
+    h = fnv(h, hw[HF_AFRONT * N]);
     const uint32_t cc = S.ccount[gi];
     h = fnv(h, cc);
     if (S.SC) {
@@ -1408,14 +1419,14 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       }
     }
     const uint2* ar = arena_of(S, gi);
-    const uint32_t base = S.abase[gi], len = S.len[gi];
+    const uint32_t base = hw[HF_ABASE * N], len = hw[HF_LEN * N];
     for (uint32_t i = 0; i < len; ++i) {
       const uint2 e = ar[(base + i) % S.A];
       h = fnv(h, e.x);
       h = fnv(h, e.y);
     }
   }
-  for (int i = 0; i < 5; ++i) h = fnv(h, S.cl[c * 8 + i]);
+  for (int i = 0; i < 5; ++i) h = fnv(h, hot_cl(S, c)[i]);
   out[ci] = h;
 }
 

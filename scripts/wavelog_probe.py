@@ -13,8 +13,8 @@ from raftsim._backend import Backend  # noqa: E402
 lib = sys.argv[1]
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 sim = Backend(lib, "raft_sim_", n_clusters=C, nodes=5, seed=42)
-sim.step(10000)
-sim.step(10000)
+for _ in range(4):                              # steady state: the bench's timed steps
+    sim.step(10000)
 waves = 2 * C // 12 + 1000                     # >= the padded packing's grid
 buf = (ctypes.c_uint32 * (waves * 8))()
 n = sim._lib.raftsim_diag_wavelog(sim._h, buf, waves)
