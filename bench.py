@@ -43,7 +43,7 @@ TICKS_PER_STEP = 10000
 FAULTS = dict(drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
 WORKLOADS = {
     # name: (config, clusters, per-rank scaling, CPU sample (clusters, steps), description)
-    "c2": (dict(nodes=5, seed=42), 65536, "weak", (65536, 10),
+    "c2": (dict(nodes=5, seed=42), 65536, "weak", (65536, 40),
            "C2: 65,536 five-node clusters per GPU x 10,000 ticks per step, no faults, no client"),
     "c3": (dict(nodes=5, seed=1, log_cap=256, client_ppm=80000, client_period=16384,
                 client_burst=2048, client_redirects=4, **FAULTS), 1 << 20, "strong", (131072, 3),

@@ -252,7 +252,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     }
 #ifdef RS_WAVELOG
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
-                          (size_t)rs::sched_slots_bound(s->C, s->N) * 32 / (64 / s->N), s->stream));
+                          (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
 #endif
     HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1]));
     done += nt;
@@ -873,7 +873,7 @@ extern "C" int raftsim_diag_wavelog(raft_sim_t* r, uint32_t* out, uint32_t cap_w
   const uint32_t waves = rs::sched_slots_bound(s->C, s->N) / (64 / s->N);
   const uint32_t n = std::min(waves, cap_waves);
   HIP_OK(hipSetDevice(s->cfg.device));
-  HIP_OK(hipMemcpy(out, s->d.wavelog, (size_t)n * 32, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(out, s->d.wavelog, (size_t)n * 128, hipMemcpyDeviceToHost));
   return (int)n;
 }
 #endif

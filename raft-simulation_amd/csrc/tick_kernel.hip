@@ -358,6 +358,9 @@ constexpr size_t block_lds_bytes() {
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
 #endif
+#ifndef RS_DRAIN   // 0: no append-response drain (A/B builds)
+#define RS_DRAIN 1
+#endif
 
 // RAFT_SCHED_ALIGNED packing key of a node: its next event (deadline or queue head).
 __device__ __forceinline__ uint32_t sched_key_of(uint32_t deadline, const QueueR& rq,
@@ -444,18 +447,28 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return wave_min(active ? min(m, cnext) : INF);
   };
   uint32_t wnext = next_event();
-#ifdef RS_PRIO   // experiment: waves that have run many active ticks issue first on their SIMD
-  uint32_t nact = 0;
-#endif
 #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
   const uint64_t wl_start = wall_clock64();
-  uint32_t wl_active = 0, wl_first = INF;
+  uint32_t wl_active = 0, wl_first = INF, wl_drain = 0;
   uint32_t wl_kmin = INF, wl_kmax = 0;
   {
     const uint32_t key = (active && k0 == 0 && S.skey) ? S.skey[c] : INF;
     wl_kmin = wave_min(key);
     wl_kmax = ~wave_min(key == INF ? ~0u : ~key);
   }
+  // per-phase shader cycles summed over the wave's active ticks: loop top + P0, P1 up to the
+  // popped message's first use, P1 handler, P1 timer/trace/counters, redirect, emission, P2, P3,
+  // P4
+  uint32_t wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t wl_ts = 0;
+#define RS_PHASE(i)                                          \
+  do {                                                       \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+    wl_ph[i] += (uint32_t)(now_ - wl_ts);                    \
+    wl_ts = now_;                                            \
+  } while (0)
+#else
+#define RS_PHASE(i) do {} while (0)
 #endif
 
   const uint32_t tend = t0 + nt;
@@ -465,6 +478,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // the wave jumps over them: discrete-event skipping with tick-exact results.
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
+#ifdef RS_WAVELOG
+    wl_ts = __builtin_amdgcn_s_memtime();
+#endif
     const bool live = active && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
     // address and shuffle index the active-tick phases use out of the tick loop, where each would
@@ -514,6 +530,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_PHASE(0);
     // ---------------------------------------------------------------- P1 one event per node
     const bool req_ok = live && (dcs || n.rq.arr <= t);
     const bool res_ok = live && n.rs.arr <= t;
@@ -587,6 +604,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
       const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
                      mpoff = m1.w;
+#ifdef RS_WAVELOG
+      asm volatile("" ::"v"(hdr), "v"(mb));   // the pop's wait lands before the stamp
+#endif
+      RS_PHASE(1);
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
                      mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
       if constexpr (TRACE) {
@@ -774,6 +795,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
       }
       const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
+      RS_PHASE(2);
       if (fault) {                                   // D8: halted with the pre-event state
         n.fault = fault;
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
@@ -819,6 +841,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           lctr_add(lctr, RAFT_CTR_LEADERS, 1);
           n.led = n.term;
         }
+        RS_PHASE(7);
         // ------------------------------------------------ redirect-client (server.clj:62-63)
         // to the :leader-id, else (rand-nth cluster) by w2 of the EVENT draw (core.clj:153-155);
         // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
@@ -847,6 +870,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             sentmask |= 1u << dst;
           }
         }
+        RS_PHASE(8);
         // ------------------------------------------------ emission (rpc / respond)
         if (emit) {
           bool part = false;
@@ -861,9 +885,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           if (emit == 3) {
             uint32_t* cl =
                 mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
+            RS_PHASE(9);
             cell_put(cl, ra, rb);
             transmit<N>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
+            RS_PHASE(10);
           } else {
+            RS_PHASE(9);
             // Message words first, for every peer at once: the next-index loads (and then the
             // prev-entry loads) of all peers are independent, so they overlap instead of paying
             // one memory round trip per peer; the fault draws follow in a compact loop.
@@ -904,6 +931,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               }
               cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
             }
+            RS_PHASE(11);
             if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
@@ -912,11 +940,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                           mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, sentmask,
                           lctr);
             }
+            RS_PHASE(10);
           }
         }
       }
     }
 
+    RS_PHASE(3);
     // ---------------------------------------------------------------- P2 network delivery
     if (__ballot(sentmask != 0)) {
       // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
@@ -954,6 +984,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_PHASE(4);
     // ---------------------------------------------------------------- P3 log writes
     // m entries were added at position n.len - m (appended_at, -1 when none)
     const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
@@ -1004,6 +1035,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
     }
 
+    RS_PHASE(5);
     // ---------------------------------------------------------------- P4 invariant checker
     // the majority-match scan can raise hwm only when the leader's log reaches past it
     const bool mcheck = (elected || mchg) && n.len > hidx;
@@ -1085,17 +1117,84 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
       }
     }
-    wnext = next_event();
-#ifdef RS_PRIO
-    ++nact;
-    if (nact == RS_PRIO) __builtin_amdgcn_s_setprio(1);
-    if (nact == RS_PRIO + 4) __builtin_amdgcn_s_setprio(2);
-    if (nact == RS_PRIO + 8) __builtin_amdgcn_s_setprio(3);
-#endif
+    RS_PHASE(6);
 #ifdef RS_WAVELOG
     ++wl_active;
     wl_first = wl_first == INF ? t - t0 : wl_first;
 #endif
+
+    // ------------------------------------------------------- append-response drain (faithful)
+    // A leader answers each append-response with no message, no log write and -- while its log
+    // does not reach past the checker's high-water mark -- no check: the event touches its own
+    // words only (core.clj:141-149, timer 171-174). Ticks at which the wave's only events are
+    // such responses are therefore run here without P0 and P2-P4, one response per leader per
+    // tick as above, until the wave's next other event E (the REQ head and client-set of every
+    // lane, and the deadline and RES head of every lane that is not a live leader). A tick at
+    // which a leader's event is anything else (a heartbeat, or a head message that is not such
+    // a response) ends the drain before that tick; the loop above then runs it. Steady state: a
+    // heartbeat round's four responses at the leader take one trip through here, not four ticks.
+    // Only where it pays: clusters of up to five nodes without client traffic (C2; with client
+    // traffic the wave has an event nearly every tick, measured C3 +3 %), and it would cost the
+    // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
+    if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (!S.client_ppm) {
+      // leaders whose responses can drain: a log past the hwm makes a success response a
+      // checker event (C3/C4 replication), so those leaders stay with the loop
+      const bool elig = active && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
+      const uint32_t oth = (!active || n.fault) ? INF
+                           : elig ? min(n.rq.arr, cnext)
+                                  : min(min(n.deadline, n.rq.arr), min(n.rs.arr, cnext));
+      const uint32_t E = __ballot(elig && n.rs.c) ? min(wave_min(oth), tend) : t;
+      if (E > t + 1 && __ballot(elig && n.rs.arr < E)) {
+        const uint32_t* qb = qslots(S, sgi, 1);
+        const size_t qs = qstride(S);
+        for (;;) {
+          const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
+          const uint32_t tau = max(wave_min(nxt), t + 1);
+          if (tau >= E) break;
+          const bool ev = elig && n.rs.arr <= tau;          // a ready message beats the timer
+          const bool hbeat = elig && !ev && n.deadline <= tau;
+          uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
+          uint32_t narr = INF;
+          const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
+          if (ev) {
+            const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
+            m0 = sp[0];
+            m1 = sp[1];
+            if (n.rs.c > 1) narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
+          }
+          const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
+          const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
+                              (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
+          if (__ballot(hbeat || (ev && !simple))) break;   // that tick is the loop's to run
+          if (ev) {
+            QueueR r = n.rs;
+            r.h = nh;
+            r.c -= 1;
+            r.arr = r.c ? narr : INF;
+            r.tail = r.c ? r.tail : 0u;
+            if (!r.c) r.h = 0;
+            n.rs = r;
+            if (flag) {                                  // append-response-handler 145-149
+              n.lsp = 1;
+              n.keys |= 1u << src;
+              lsw.next(src - 1) = (int32_t)m1.x;
+              lsw.match(src - 1) = (int32_t)m0.w;
+            } else {                                     // 143-144: (dec next-index)
+              lsw.next(src - 1) -= 1;
+            }
+            n.deadline = tau + S.hb;
+            n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
+                                  n.term, 0);
+            lctr_add(lctr, RAFT_CTR_EV_AR, 1);
+          }
+          t = tau;
+#ifdef RS_WAVELOG
+          ++wl_drain;
+#endif
+        }
+      }
+    }
+    wnext = next_event();
   }
 #ifdef RS_WAVELOG
   if (lane == 0 && S.wavelog) {
@@ -1103,10 +1202,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 8);
+    uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 32);
     rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
                         (uint32_t)(wl_end >> 32));
     rec[1] = make_uint4(wl_active, hw, xcc, (wl_kmax - wl_kmin) << 16 | (wl_first & 0xFFFF));
+    rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
+    rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
+    rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
+    rec[5] = make_uint4(wl_drain, 0, 0, 0);
   }
 #endif
 

@@ -16,9 +16,9 @@ sim = Backend(lib, "raft_sim_", n_clusters=C, nodes=5, seed=42)
 for _ in range(4):                              # steady state: the bench's timed steps
     sim.step(10000)
 waves = 2 * C // 12 + 1000                     # >= the padded packing's grid
-buf = (ctypes.c_uint32 * (waves * 8))()
+buf = (ctypes.c_uint32 * (waves * 32))()
 n = sim._lib.raftsim_diag_wavelog(sim._h, buf, waves)
-a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 8)[:n].astype(np.int64)
+a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 32)[:n].astype(np.int64)
 a = a[(a[:, 0] | a[:, 1]) != 0]                 # waves that ran (padding waves exit first)
 n = len(a)
 start = (a[:, 0] | (a[:, 1] << 32)); end = (a[:, 2] | (a[:, 3] << 32))
@@ -61,3 +61,10 @@ b = np.array(list(busy.values()))
 print("per-SIMD summed wave-us p0/50/100:", b.min(), np.median(b), b.max())
 per_xcc = [np.median(life[xcc == x]) for x in range(8)]
 print("per-XCC median life:", " ".join(f"{v:.1f}" for v in per_xcc))
+ph = a[:, [8, 9, 10, 15, 16, 17, 19, 18, 11, 12, 13, 14]].astype(np.float64)
+tot = ph.sum(axis=1)
+print("phase cycles per active tick (mean over waves): " + "  ".join(
+    f"{nm} {v:7.0f}" for nm, v in zip(("top+P0", "P1pop", "P1hdl", "P1timer", "P1redir", "emit-pre", "bcast-cells", "cells-xmit", "emit-post", "P2", "P3", "P4+next"),
+                                      (ph / np.maximum(act, 1)[:, None]).mean(axis=0))))
+print("drained ticks per wave p0/10/50/90/99/100:", q(a[:, 20]))
+print(f"stamped cycles / lifetime cycles (2.4 GHz nominal): {np.median(tot / (life * 2400)):.2f}")
