@@ -108,14 +108,12 @@ def main():
         "bench_avg_launch_ms_hip_events": roof["avg_launch_ms"],
         "vgpr": next((r.get("VGPR_Count") for r in trace if KERNEL in r["Kernel_Name"]), None),
         "pmc_per_launch": avg,
-        # occupancy and clock (MI355X_MICROARCH.md: SQ_WAVE_CYCLES in quad-cycles summed over
-        # waves; GRBM_GUI_ACTIVE summed over the 8 XCDs): mean resident waves per CU over the
-        # launch, and the effective shader clock
+        # occupancy (MI355X_MICROARCH.md: SQ_WAVE_CYCLES in quad-cycles summed over waves;
+        # GRBM_GUI_ACTIVE summed over the 8 XCDs): mean resident waves per CU over the
+        # launch
         "derived": {
             "mean_waves_per_cu": 4 * avg["SQ_WAVE_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 256)
             if avg.get("GRBM_GUI_ACTIVE") and "SQ_WAVE_CYCLES" in avg else None,
-            "effective_clock_GHz": avg["GRBM_GUI_ACTIVE"] / 8 / avg_ns
-            if avg.get("GRBM_GUI_ACTIVE") else None,
             "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
             if avg.get("SQ_WAVES") and "SQ_INSTS_VALU" in avg else None},
         "calibration": {"k_read": k_rd, "k_write": k_wr, "state_read_weight": w_state,

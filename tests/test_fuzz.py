@@ -48,3 +48,41 @@ def test_fuzz_gpu_equals_oracle(seed):
         assert not len(bad), (f"tick {g.tick - 1}: {len(bad)} clusters differ; first {bad[0]}\n"
                               + helpers.describe_cluster_diff(g, r, int(bad[0])))
     assert g.counters() == r.counters()
+
+
+def _gpu_vs_oracle_multi_tick(cfg, scns, steps):
+    g = fuzz.load_batch(helpers.gpu, cfg, scns)
+    r = fuzz.load_batch(helpers.oracle, cfg, scns)
+    for n in steps:
+        g.step(n)
+        r.step(n)
+        dg, dr = g.digest(), r.digest()
+        bad = np.nonzero(dg != dr)[0]
+        assert not len(bad), (f"after tick {g.tick}: {len(bad)} clusters differ; first {bad[0]}\n"
+                              + helpers.describe_cluster_diff(g, r, int(bad[0])))
+    assert g.counters() == r.counters()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_gpu_multi_tick_launch(seed):
+    """The same random states stepped several ticks per launch: idle-tick skipping and the
+    append-response drain (which need a launch longer than one tick) against the oracle."""
+    rng = random.Random(7000 + seed)
+    cfg = fuzz.random_config(rng)
+    scns = [fuzz.random_scenario(rng, cfg) for _ in range(200)]
+    _gpu_vs_oracle_multi_tick(cfg, scns, [8, 5, 40])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_gpu_drain(seed):
+    """Configurations where the append-response drain runs (faithful model, N <= 5, no client
+    traffic, no trace rings), random states with queued responses, short timers (hb 1..6, so a
+    leader's heartbeat falls inside a drain), with and without faults."""
+    rng = random.Random(9000 + seed)
+    cfg = fuzz.random_config(rng)
+    cfg.update(nodes=rng.randint(2, 5), variant_flags=rng.choice([0, 1]), client_ppm=0,
+               trace_cap=0, trace_entry_cap=0)
+    scns = [fuzz.random_scenario(rng, cfg) for _ in range(200)]
+    _gpu_vs_oracle_multi_tick(cfg, scns, [8, 8, 64, 200])
