@@ -9,8 +9,8 @@
 //                    A wave's clusters come from the packing permutation, i.e. from anywhere in
 //                    the shard: a block per cluster makes the wave's state load touch only its own
 //                    clusters' lines (the structure-of-arrays layout read ~13 lines per load)
-//   queues           qbuf[which][slot][gi] of 8-word messages (ring per node, sorted by arrival);
-//                    slot-major so the same ring slot of a cluster's nodes is contiguous
+//   queues           8-word messages, one ring per node and queue, sorted by arrival: REQ rings
+//                    slot-major qbuf[0][slot][gi], RES rings node-major qbuf[1][gi][slot] (qslots)
 //   log arenas       arena[gi][A] of (term, val)
 //   cold node words  ccount (commit_count), commit-stream / trace rings               [NN]...
 // A wave owns floor(64 / N) whole clusters, one lane per node; a cluster never spans waves, so all
@@ -42,7 +42,7 @@ struct DevSim {
       client_ppm, variant, client_period, client_burst, client_redirects;
   uint32_t* hot;          // [C][HB] cluster blocks (HotField, hot_cl_off, hot_block_words)
   uint32_t HB;            // hot_block_words(N)
-  uint32_t* qbuf;         // [2][Q][NN][8]
+  uint32_t* qbuf;         // REQ [Q][NN][8], then RES [NN][Q][8]
   uint32_t* arena;        // [NN][A][2]
   uint32_t* ccount;       // [NN] commit_count (F2)
   uint32_t* stream;       // [NN][SC] commit-stream rings (F2)
@@ -201,11 +201,16 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 
 __device__ __forceinline__ uint32_t wrapq(uint32_t x, uint32_t Q) { return x >= Q ? x - Q : x; }
 
-// Slot 0 of node gi's queue `which`; slot i is qslots(...) + i * qstride(S).
+// Slot 0 of node gi's queue `which`; slot i is qslots(...) + i * qstride(S, which). REQ rings are
+// slot-major ([slot][gi]: the followers of a cluster take their append-entries in the same tick
+// from adjacent words), RES rings node-major ([gi][slot]: a leader takes its responses one per
+// tick from consecutive slots of one line).
 __device__ __forceinline__ uint32_t* qslots(const DevSim& S, uint32_t gi, int which) {
-  return S.qbuf + ((size_t)which * S.Q * S.NN + gi) * 8;
+  return S.qbuf + (which ? (size_t)S.Q * S.NN + (size_t)gi * S.Q : (size_t)gi) * 8;
 }
-__device__ __forceinline__ size_t qstride(const DevSim& S) { return (size_t)S.NN * 8; }
+__device__ __forceinline__ size_t qstride(const DevSim& S, int which) {
+  return which ? 8 : (size_t)S.NN * 8;
+}
 
 __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
   return reinterpret_cast<uint2*>(S.arena) + (size_t)gi * S.A;
@@ -229,7 +234,7 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
     return;
   }
   uint32_t* qb = qslots(S, gi, which);
-  const size_t qs = qstride(S);
+  const size_t qs = qstride(S, which);
   const uint32_t arr = m0.x, head = q.h;
   uint32_t pos = q.c;
   if (pos > 0 && arr < q.tail) {

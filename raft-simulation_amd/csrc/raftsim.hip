@@ -296,9 +296,13 @@ static int check_range(Shard* s, uint32_t c0, uint32_t nc) {
   return 0;
 }
 
-// Slot 0 of node gi's queue `which` in the slot-major queue buffer [2][Q][NN] (slot stride NN).
+// Slot 0 of node gi's queue `which` and the ring's slot pitch in bytes (rs::qslots: REQ rings
+// slot-major, RES rings node-major).
 static uint32_t* qring(Shard* s, uint32_t gi, uint32_t which) {
-  return s->d.qbuf + ((size_t)which * s->Q * s->NN + gi) * 8;
+  return s->d.qbuf + (which ? (size_t)s->Q * s->NN + (size_t)gi * s->Q : (size_t)gi) * 8;
+}
+static size_t qpitch(Shard* s, uint32_t which) {
+  return (which ? 1 : (size_t)s->NN) * sizeof(raft_msg_t);
 }
 
 // Field `f` of node `id` in cluster `cluster`'s hot block (rs::HotField).
@@ -417,7 +421,7 @@ static int sh_read_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which
   std::vector<raft_msg_t> slots(s->Q);
   HIP_OK(d2h(s, &qm, hot_word(s, cluster, id, rs::HF_QMETA), 1));
   HIP_OK(hipMemcpy2DAsync(slots.data(), sizeof(raft_msg_t), qring(s, gi, which),
-                          (size_t)s->NN * sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q,
+                          qpitch(s, which), sizeof(raft_msg_t), s->Q,
                           hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
   const uint32_t head = which ? (qm >> 9) & 15 : qm & 15;
@@ -450,7 +454,7 @@ static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t whic
   if (which) qm = (qm & ~(0xFu << 9 | 0x1Fu << 13)) | count << 13;
   else qm = (qm & ~0x1FFu) | count << 4;
   const uint32_t harr = count ? in[0].arrival : rs::INF, tail = count ? in[count - 1].arrival : 0;
-  HIP_OK(hipMemcpy2DAsync(qring(s, gi, which), (size_t)s->NN * sizeof(raft_msg_t), slots.data(),
+  HIP_OK(hipMemcpy2DAsync(qring(s, gi, which), qpitch(s, which), slots.data(),
                           sizeof(raft_msg_t), sizeof(raft_msg_t), s->Q, hipMemcpyHostToDevice,
                           s->stream));
   HIP_OK(h2d(s, hot_word(s, cluster, id, rs::HF_QMETA), &qm, 1));

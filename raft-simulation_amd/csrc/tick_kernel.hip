@@ -576,7 +576,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // the ring is always in bounds) and used only when the queue stays non-empty.
         const QueueR q = which ? n.rs : n.rq;
         const uint32_t* qb = qslots(S, sgi, which);
-        const size_t qs = qstride(S);
+        const size_t qs = qstride(S, which);
         const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
         m0 = sp[0];
         m1 = sp[1];
@@ -1146,7 +1146,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       const uint32_t E = __ballot(elig && n.rs.c) ? min(wave_min(oth), tend) : t;
       if (E > t + 1 && __ballot(elig && n.rs.arr < E)) {
         const uint32_t* qb = qslots(S, sgi, 1);
-        const size_t qs = qstride(S);
+        const size_t qs = qstride(S, 1);
         for (;;) {
           const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
           const uint32_t tau = max(wave_min(nxt), t + 1);
@@ -1517,7 +1517,7 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       h = fnv(h, qc[which]);
       const uint32_t* qb = qslots(S, gi, which);
       for (uint32_t i = 0; i < qc[which]; ++i) {
-        const uint32_t* m = qb + ((qh[which] + i) % S.Q) * qstride(S);
+        const uint32_t* m = qb + ((qh[which] + i) % S.Q) * qstride(S, which);
         for (int j = 0; j < 8; ++j) h = fnv(h, m[j]);
       }
     }
