@@ -449,7 +449,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   uint32_t wnext = next_event();
 #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
   const uint64_t wl_start = wall_clock64();
-  uint32_t wl_active = 0, wl_first = INF, wl_drain = 0;
+  uint32_t wl_active = 0, wl_first = INF, wl_drain = 0, wl_inj = 0, wl_dead = 0;
+  {
+    const uint64_t fm = __ballot(active && n.fault);
+    const uint32_t all = (1u << N) - 1;
+    wl_dead = __popcll(__ballot(active && k0 == 0 && ((uint32_t)(fm >> bl0) & all) == all));
+  }
   uint32_t wl_kmin = INF, wl_kmax = 0;
   {
     const uint32_t key = (active && k0 == 0 && S.skey) ? S.skey[c] : INF;
@@ -505,6 +510,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     bool inj = false;
     uint32_t injv = 0;
     const bool cinj = active && t == cnext;
+#ifdef RS_WAVELOG
+    wl_inj += __ballot(cinj) ? 1 : 0;
+#endif
     if (__ballot(cinj)) {
       if (cinj) {
         const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
@@ -1209,7 +1217,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
     rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
     rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
-    rec[5] = make_uint4(wl_drain, 0, 0, 0);
+    rec[5] = make_uint4(wl_drain, wl_inj, wl_dead, 0);
   }
 #endif
 

@@ -1,5 +1,6 @@
 """Per-wave timeline of one C2 launch from a -DRS_WAVELOG build (diagnostic only): lifetime
-distribution, start-time generations, per-CU/SIMD packing. Usage: wavelog_probe.py LIB [clusters]"""
+distribution, start-time generations, per-CU/SIMD packing.
+Usage: wavelog_probe.py LIB [clusters] [c2|c3]"""
 import ctypes
 import sys
 from pathlib import Path
@@ -12,7 +13,12 @@ from raftsim._backend import Backend  # noqa: E402
 
 lib = sys.argv[1]
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-sim = Backend(lib, "raft_sim_", n_clusters=C, nodes=5, seed=42)
+WL = sys.argv[3] if len(sys.argv) > 3 else "c2"
+CFG = {"c2": dict(nodes=5, seed=42),
+       "c3": dict(nodes=5, seed=1, log_cap=256, client_ppm=80000, client_period=16384,
+                  client_burst=2048, client_redirects=4, drop_ppm=100000, dup_ppm=10000, dmin=1,
+                  dmax=50, part_ppm=100000)}[WL]
+sim = Backend(lib, "raft_sim_", n_clusters=C, **CFG)
 for _ in range(4):                              # steady state: the bench's timed steps
     sim.step(10000)
 waves = 2 * C // 12 + 1000                     # >= the padded packing's grid
@@ -67,4 +73,6 @@ print("phase cycles per active tick (mean over waves): " + "  ".join(
     f"{nm} {v:7.0f}" for nm, v in zip(("top+P0", "P1pop", "P1hdl", "P1timer", "P1redir", "emit-pre", "bcast-cells", "cells-xmit", "emit-post", "P2", "P3", "P4+next"),
                                       (ph / np.maximum(act, 1)[:, None]).mean(axis=0))))
 print("drained ticks per wave p0/10/50/90/99/100:", q(a[:, 20]))
+print("client-injection ticks per wave p0/10/50/90/99/100:", q(a[:, 21]))
+print("dead clusters per wave at launch start p0/10/50/90/99/100:", q(a[:, 22]))
 print(f"stamped cycles / lifetime cycles (2.4 GHz nominal): {np.median(tot / (life * 2400)):.2f}")
