@@ -34,7 +34,12 @@ constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min v
 constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
 static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
-constexpr int PW_WORDS = 64;   // 32 x u64 client-gap powers at the start of the block's LDS
+constexpr int PW_WORDS = 64;
+// Waves flush their counters into one of CTR_COPIES copies of the counter block (wave index mod
+// CTR_COPIES): thousands of waves ending together otherwise serialise on the same few words of
+// device-scope atomics (C2: 5,724 waves x up to 30 counters). The host reduces the copies.
+constexpr int CTR_COPIES = 64;
+constexpr int CTR_STRIDE = RAFT_CTR_COUNT + 2;   // 32 x u64 client-gap powers at the start of the block's LDS
 
 struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
@@ -54,7 +59,8 @@ struct DevSim {
   uint32_t TC, TE;
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
   int client_top;                       // highest i with client_pw[i] > 0, -1 if none
-  unsigned long long* ctr;  // [RAFT_CTR_COUNT] sums, [+0] first violation (min), [+1] payload (max)
+  unsigned long long* ctr;  // [CTR_COPIES][CTR_STRIDE]: [RAFT_CTR_COUNT] sums, then the first
+                            // violation (min) and the largest payload (max); summed by the host
   const uint32_t* perm;     // [slots] wave slot -> cluster or INF (RAFT_SCHED_ALIGNED), null = identity
   const uint32_t* nslots;   // RAFT_SCHED_ALIGNED: slots in use this launch (device word)
   uint32_t* skey;           // [C] RAFT_SCHED_ALIGNED: cluster's next event - next launch's t0
@@ -217,7 +223,9 @@ __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
 }
 
 __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
+#ifndef RS_COST_NOCTR   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
   if (v) atomicAdd(&lctr[i], v);
+#endif
 }
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own

@@ -104,6 +104,14 @@ static int validate_cfg(const raft_sim_config_t* c) {
   return 0;
 }
 
+// Zero every copy of the counter block, with "no violation" (UINT64_MAX) in the first-violation
+// slots (rs::CTR_COPIES copies of rs::CTR_STRIDE words, reduced by sh_read_counters).
+static hipError_t init_counters(Shard* s) {
+  std::vector<unsigned long long> c((size_t)rs::CTR_COPIES * rs::CTR_STRIDE, 0ull);
+  for (int k = 0; k < rs::CTR_COPIES; ++k) c[(size_t)k * rs::CTR_STRIDE + RAFT_CTR_COUNT] = ~0ull;
+  return hipMemcpy(s->d.ctr, c.data(), c.size() * 8, hipMemcpyHostToDevice);   // blocking: c dies
+}
+
 template <typename T>
 static int dalloc(Shard* s, T** p, size_t count) {
   void* v = nullptr;
@@ -166,7 +174,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   if ((rc = dalloc(s, &d.hot, (size_t)s->C * d.HB)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
       (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) ||
-      (rc = dalloc(s, &d.ctr, RAFT_CTR_COUNT + 2)) || (rc = dalloc(s, &s->client_pw, 32)) ||
+      (rc = dalloc(s, &d.ctr, (size_t)rs::CTR_COPIES * rs::CTR_STRIDE)) || (rc = dalloc(s, &s->client_pw, 32)) ||
       (rc = dalloc(s, &d.ccount, NN)) ||
       (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1))) ||
       (rc = dalloc(s, &d.tr, NN * std::max<uint32_t>(d.TC, 1) * 32)) ||
@@ -200,7 +208,6 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
       (e = hipMemsetAsync(d.hot, 0, (size_t)s->C * d.HB * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
-      (e = hipMemsetAsync(d.ctr, 0, RAFT_CTR_COUNT * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.stream, 0, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1) * 4,
                           s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tr, 0, NN * std::max<uint32_t>(d.TC, 1) * 128, s->stream)) != hipSuccess ||
@@ -208,8 +215,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
       (e = hipMemsetAsync(d.tent, 0, NN * std::max<uint32_t>(d.TE, 1) * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tecount, 0, NN * 4, s->stream)) != hipSuccess ||
       (d.shist && (e = hipMemsetAsync(d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream)) != hipSuccess) ||
-      (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT, 0xFF, 8, s->stream)) != hipSuccess ||
-      (e = hipMemsetAsync(d.ctr + RAFT_CTR_COUNT + 1, 0, 8, s->stream)) != hipSuccess ||
+      (e = init_counters(s)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
       (e = rs::launch_init(d, s->stream)) != hipSuccess ||
@@ -607,12 +613,18 @@ static int sh_write_clusters(Shard* s, uint32_t c0, uint32_t nc, const raft_clus
 static int sh_read_counters(Shard* s, raft_counters_t* out) {
   if (!s || !out) return fail(-EINVAL, "null argument");
   HIP_OK(hipSetDevice(s->cfg.device));
-  unsigned long long buf[RAFT_CTR_COUNT + 2];
-  HIP_OK(hipMemcpyAsync(buf, s->d.ctr, sizeof buf, hipMemcpyDeviceToHost, s->stream));
+  std::vector<unsigned long long> buf((size_t)rs::CTR_COPIES * rs::CTR_STRIDE);
+  HIP_OK(hipMemcpyAsync(buf.data(), s->d.ctr, buf.size() * 8, hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
-  for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] = buf[i];
-  out->first_violation_tick = buf[RAFT_CTR_COUNT];
-  out->payload_max = buf[RAFT_CTR_COUNT + 1];
+  memset(out->c, 0, sizeof out->c);
+  out->first_violation_tick = ~0ull;
+  out->payload_max = 0;
+  for (int k = 0; k < rs::CTR_COPIES; ++k) {        // the copies the waves flushed into
+    const unsigned long long* b = &buf[(size_t)k * rs::CTR_STRIDE];
+    for (int i = 0; i < RAFT_CTR_COUNT; ++i) out->c[i] += b[i];
+    out->first_violation_tick = std::min<uint64_t>(out->first_violation_tick, b[RAFT_CTR_COUNT]);
+    out->payload_max = std::max<uint64_t>(out->payload_max, b[RAFT_CTR_COUNT + 1]);
+  }
   out->node_ticks = (uint64_t)s->NN * s->ticks_run;
   return 0;
 }

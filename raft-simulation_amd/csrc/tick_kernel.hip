@@ -20,6 +20,9 @@ __device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) 
 __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t ev, uint32_t src,
                                                 uint32_t mterm, uint32_t role, uint32_t term,
                                                 uint32_t fault) {
+#ifdef RS_COST_NOTRACE   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
+  return h ^ t;
+#endif
   h = fnv(h, t);
   h = fnv(h, ev);
   h = fnv(h, src);
@@ -27,6 +30,15 @@ __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t
   h = fnv(h, role);
   h = fnv(h, term);
   return fnv(h, fault);
+}
+
+// The EVENT draw of node id at tick t (SIM_SPEC §3): alts!! bit, timeout, rand-nth peer.
+__device__ __forceinline__ uint4 event_draw(uint32_t g, uint32_t id, uint32_t t, const DevSim& S) {
+#ifdef RS_COST_NOPHILOX   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
+  const uint32_t x = (g * 0x9E3779B9u) ^ (id * 0x85EBCA6Bu) ^ (t * 0xC2B2AE35u);
+  return make_uint4(x, x * 0x27D4EB2Fu, x ^ (x >> 15), x + 0x165667B1u);
+#endif
+  return philox(g, id | P_EVENT << 8, t, 0, S.key0, S.key1);
 }
 
 // LDS message cells. A node emits either one broadcast or one reply per tick, and the words
@@ -559,7 +571,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       bool have_w = false;
       int which = -1;
       if (req_ok && res_ok) {
-        w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+        w = event_draw(sg, id, t, S);
         have_w = true;
         which = (w.x & 1) ? 1 : 0;
       } else if (req_ok) {
@@ -595,7 +607,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         uint32_t narr = INF;
         if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
         if (!have_w && n.role != RAFT_LEADER) {
-          w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+          w = event_draw(sg, id, t, S);
           have_w = true;
         }
         QueueR r = q;
@@ -818,7 +830,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (n.role == RAFT_LEADER) {
           if (!SPEC || ev == 7 || elected) n.deadline = t + S.hb;
         } else if (!SPEC || ev == 6 || rearm || was_leader) {
-          if (!have_w) w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+          if (!have_w) w = event_draw(sg, id, t, S);
           have_w = true;
           n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
         }
@@ -842,7 +854,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           lsw.next(src - 1) = (int32_t)(SPEC ? mb + 1 : mb);
           lsw.match(src - 1) = (int32_t)(SPEC ? mb : ma);
         }
+#ifndef RS_COST_NOEVCTR   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
         lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
+#endif
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
         lctr_add(lctr, RAFT_CTR_ENTRIES_APPLIED, applied);
         if (elected) {
@@ -862,7 +876,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           } else {
             uint32_t dst = n.lid;
             if (!dst) {
-              if (!have_w) w = philox(sg, id | P_EVENT << 8, t, 0, S.key0, S.key1);
+              if (!have_w) w = event_draw(sg, id, t, S);
               const uint32_t i = __umulhi(w.z, N - 1);
               dst = i + 1 < id ? i + 1 : i + 2;
             }
@@ -1257,15 +1271,16 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  unsigned long long* const ctr = S.ctr + (size_t)(wave % CTR_COPIES) * CTR_STRIDE;
   if (lane < RAFT_CTR_COUNT) {
     const uint32_t v = lctr[lane];
-    if (v) atomicAdd(&S.ctr[lane], (unsigned long long)v);
+    if (v) atomicAdd(&ctr[lane], (unsigned long long)v);
   } else if (lane == LCTR_FIRSTVIOL) {
     const uint32_t v = lctr[lane];
-    if (v != INF) atomicMin(&S.ctr[RAFT_CTR_COUNT], (unsigned long long)v);
+    if (v != INF) atomicMin(&ctr[RAFT_CTR_COUNT], (unsigned long long)v);
   } else if (lane == LCTR_PAYLOADMAX) {
     const uint32_t v = lctr[lane];
-    if (v) atomicMax(&S.ctr[RAFT_CTR_COUNT + 1], (unsigned long long)v);
+    if (v) atomicMax(&ctr[RAFT_CTR_COUNT + 1], (unsigned long long)v);
   }
 }
 
