@@ -1243,9 +1243,15 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t cm = active ? cnext : INF;
 #pragma unroll
     for (int s = 0; s < N; ++s) cm = min(cm, (uint32_t)__shfl(me, bl0 + s));
-    if (active && k0 == 0) {
-      const uint32_t key = sched_bucket(cm, tend);
-      S.skey[c] = key;
+    const bool head = active && k0 == 0;
+    const uint32_t key = head ? sched_bucket(cm, tend) : INF;
+    if (head) S.skey[c] = key;
+    // a packed wave's clusters usually share their next key: one histogram atomic for the wave
+    const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
+    const uint32_t heads = (uint32_t)__popcll(__ballot(head));   // (ballot outside any branch)
+    if (kmin == kmax) {
+      if (lane == 0 && kmin != INF) atomicAdd(&S.shist[kmin], heads);
+    } else if (head) {
       atomicAdd(&S.shist[key], 1u);
     }
   }
