@@ -252,8 +252,8 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       s->keys_fresh = true;
     }
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
-      hipEvent_t e;
-      HIP_OK(hipEventCreate(&e));
+      hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
       s->kev.push_back(e);
     }
 #ifdef RS_WAVELOG
