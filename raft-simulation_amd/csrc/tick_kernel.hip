@@ -125,6 +125,30 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
+// Log Matching over cnt consecutive positions of two logs whose first slots are xi in arena xa
+// and yi in arena ya (slots wrap at A): is there a position with the same term and a different
+// value? Four positions per trip with their eight loads in flight together (a 2000-entry
+// AppendEntries is checked against every peer: one memory round trip per entry was most of C4's
+// time); every slot read is inside the arena, the comparisons past cnt are masked.
+__device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
+                                             uint32_t yi, uint32_t cnt, uint32_t A) {
+  for (uint32_t i = 0; i < cnt; i += 4) {
+    uint2 x[4], y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = xa[xi];
+      y[j] = ya[yi];
+      xi = xi + 1 == A ? 0 : xi + 1;
+      yi = yi + 1 == A ? 0 : yi + 1;
+    }
+    bool c = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c |= i + j < cnt && x[j].x == y[j].x && x[j].y != y[j].y;
+    if (c) return true;
+  }
+  return false;
+}
+
 // Copy `cnt` arena entries from slot si of `src` to slot di of `dst` (slots wrap at A), eight per
 // batch: a batch's loads are all issued before its stores, so a long copy pays one memory round
 // trip per eight entries rather than one per entry. Ascending order with every load of a batch
@@ -1071,7 +1095,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
         if (bad) violation(lctr, RAFT_CTR_VIOL_ELECTION, t);
       }
+#ifdef RS_COST_NOLOGCHECK   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
+      if (false) {
+#else
       if (__ballot(appended_at >= 0)) {              // log matching
+#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
         bool bad = false;
 #pragma unroll
@@ -1079,14 +1107,9 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           const uint32_t sb = __shfl(n.base, bl + s), sl = __shfl(n.len, bl + s);
           if (appended_at >= 0 && s != k && !bad) {
             const uint2* oa = arena_of(S, sgi - k + s);
-            const uint32_t hi = n.len < sl ? n.len : sl;
-            for (uint32_t p = (uint32_t)appended_at; p < hi; ++p) {
-              const uint2 x = sar[(n.base + p) % A], y = oa[(sb + p) % A];
-              if (x.x == y.x && x.y != y.y) {
-                bad = true;
-                break;
-              }
-            }
+            const uint32_t hi = n.len < sl ? n.len : sl, lo = (uint32_t)appended_at;
+            if (hi > lo)
+              bad = log_conflict(sar, (n.base + lo) % A, oa, (sb + lo) % A, hi - lo, A);
           }
         }
         if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
