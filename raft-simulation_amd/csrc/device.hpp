@@ -132,14 +132,20 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
 }
 
 // Geometric gap G(w) of SIM_SPEC §4 P0: the greedy power search over pw[top..0] (higher powers
-// are 0 and never fire).
+// are 0 and never fire). The accumulator starts at 2^32 and every power is below 2^32 when
+// client_ppm > 0 (the only case the gap is drawn for), so after its first step it fits 32 bits
+// and (acc * pw) >> 32 is one v_mul_hi_u32 instead of a 64x64-bit product.
 __device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
   const uint64_t u = (uint64_t)w + 1;
-  uint64_t acc = 1ull << 32, g = 0;
+  uint32_t acc = 0;
+  bool full = true;                 // acc == 2^32
+  uint64_t g = 0;
   for (int i = top; i >= 0; --i) {
-    const uint64_t c = (acc * pw[i]) >> 32;
-    if (c >= u) {
+    const uint32_t p = (uint32_t)pw[i];
+    const uint32_t c = full ? p : __umulhi(acc, p);
+    if ((uint64_t)c >= u) {
       acc = c;
+      full = false;
       g += 1ull << i;
     }
   }

@@ -74,6 +74,9 @@ CASES = {
                         variant_flags=2, commit_stream_cap=64, **BURSTS, **FAULTS),
     "spec_nolog_bursts": dict(n_clusters=1024, nodes=5, seed=63, client_ppm=80000, log_cap=1024,
                               variant_flags=3, **BURSTS, **FAULTS),
+    # faithful crash storm under client traffic: most client-sets reach halted nodes (to-halted)
+    "crash_storm_clients": dict(n_clusters=2048, nodes=5, seed=13, client_ppm=80000, log_cap=16,
+                                hb=300, el_base=500, el_span=500, **BURSTS, **FAULTS),
     "redirect_storm": dict(n_clusters=512, nodes=6, seed=65, client_ppm=1000000,
                            client_period=300, client_burst=40, client_redirects=16, inbox_cap=4,
                            log_cap=128, hb=50, el_base=80, el_span=80, **FAULTS),

@@ -167,19 +167,31 @@ def test_commit_logs_written_like_the_reference(tmp_path):
     assert be.counters()["entries_applied"] == sum(r["commit_count"] for r in be.read_nodes())
 
 
+IDLE_CASES = {
+    "bursts": dict(n_clusters=61, nodes=5, seed=13, client_ppm=50000, drop_ppm=50000, dmax=30,
+                   part_ppm=100000, log_cap=128, client_period=5000, client_burst=700,
+                   client_redirects=3, trace_cap=64, trace_entry_cap=512),
+    # crash storm: IOOBE/OVERFLOW halts under client traffic, most client-sets reach halted nodes
+    "crash_storm": dict(n_clusters=61, nodes=5, seed=13, client_ppm=80000, drop_ppm=100000,
+                        dup_ppm=10000, dmax=50, part_ppm=100000, log_cap=16, client_period=16384,
+                        client_burst=2048, client_redirects=4, hb=300, el_base=500, el_span=500),
+}
+
+
 @pytest.mark.parametrize("variant", [0, 2])
-def test_idle_skipping_does_not_change_results(variant):
+@pytest.mark.parametrize("case", list(IDLE_CASES))
+def test_idle_skipping_does_not_change_results(case, variant):
     """The CPU baseline's discrete-event skipping visits only ticks with something due and gives
     the every-tick restatement's results exactly."""
-    cfg = dict(n_clusters=61, nodes=5, seed=13, client_ppm=50000, drop_ppm=50000, dmax=30,
-               part_ppm=100000, log_cap=128, client_period=5000, client_burst=700,
-               client_redirects=3, variant_flags=variant, trace_cap=64, trace_entry_cap=512)
+    cfg = dict(IDLE_CASES[case], variant_flags=variant)
     a, b = helpers.oracle(**cfg), helpers.oracle(**cfg)
     helpers.oracle_idle_skip(b)
-    for n in (1, 4999, 7000, 3):
+    for n in (1, 4999, 7000, 3, 9000):
         a.step(n)
         b.step(n)
         assert (a.digest() == b.digest()).all() and a.counters() == b.counters()
+    if case == "crash_storm" and variant == 0:
+        assert a.counters()["to_halted"] > a.counters()["client_injected"] // 4
 
 
 def test_threads_do_not_change_results():
