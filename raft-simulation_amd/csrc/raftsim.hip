@@ -186,7 +186,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   }
   d.client_pw = s->client_pw;
   d.wavelog = nullptr;
-#ifdef RS_WAVELOG
+#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
   if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {
     sh_destroy(s);
     return rc;
@@ -256,7 +256,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
       s->kev.push_back(e);
     }
-#ifdef RS_WAVELOG
+#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
                           (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
 #endif
@@ -880,7 +880,7 @@ int raft_sim_read_counters(raft_sim_t* r, raft_counters_t* out) {
   return 0;
 }
 
-#ifdef RS_WAVELOG
+#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
 // Diagnostic builds only (not part of include/raftsim.h): the per-wave timeline of shard 0's last
 // tick-kernel launch, 8 words per wave: start lo/hi, end lo/hi (100 MHz), active ticks, HW_ID,
 // XCC_ID, launch t0. Returns the number of waves.

@@ -378,9 +378,15 @@ constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 #endif
 template <int N>
 constexpr bool nm_lds() { return RS_NM_LDS && N <= 5; }
+#ifdef RS_REGIONCOUNT   // diagnostic build: per-wave execution counts of code regions (RS_RC)
+constexpr int RC_WORDS = 32;
+#else
+constexpr int RC_WORDS = 0;
+#endif
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
-  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0);
+  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
+         RC_WORDS;
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -431,6 +437,17 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+#ifdef RS_REGIONCOUNT
+  // region i executed by the wave (any lane active): the first active lane counts it
+  uint32_t* rcl = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
+  if (lane < RC_WORDS) rcl[lane] = 0;
+#define RS_RC(i)                                                       \
+  do {                                                                 \
+    if (lane == (int)__builtin_ctzll(__ballot(1))) rcl[i] += 1;        \
+  } while (0)
+#else
+#define RS_RC(i) do {} while (0)
+#endif
   __builtin_amdgcn_wave_barrier();
 
   const uint32_t wave = blockIdx.x;
@@ -519,6 +536,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // the wave jumps over them: discrete-event skipping with tick-exact results.
     if (t < wnext) t = wnext < tend ? wnext : tend;
     if (t == tend) break;
+    RS_RC(0);
 #ifdef RS_WAVELOG
     wl_ts = __builtin_amdgcn_s_memtime();
 #endif
@@ -550,6 +568,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     wl_inj += __ballot(cinj) ? 1 : 0;
 #endif
     if (__ballot(cinj)) {
+      RS_RC(1);
       if (cinj) {
         const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
         if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
@@ -589,12 +608,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     uint32_t pmax = 0;                                        // largest AE payload emitted
     uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
     if (live && (req_ok || res_ok || t >= n.deadline)) {
+      RS_RC(2);
       // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
       // and for the next timeout of a non-leader (core.clj:174); leaders' events skip it.
       uint4 w = make_uint4(0, 0, 0, 0);
       bool have_w = false;
       int which = -1;
       if (req_ok && res_ok) {
+        RS_RC(4);
         w = event_draw(sg, id, t, S);
         have_w = true;
         which = (w.x & 1) ? 1 : 0;
@@ -618,6 +639,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // (needed for its next timeout whatever the message does, unless it becomes leader) is
         // computed in their shadow. The next head's arrival is loaded unconditionally (a slot of
         // the ring is always in bounds) and used only when the queue stays non-empty.
+        RS_RC(3);
         const QueueR q = which ? n.rs : n.rq;
         const uint32_t* qb = qslots(S, sgi, which);
         const size_t qs = qstride(S, which);
@@ -631,6 +653,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         uint32_t narr = INF;
         if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
         if (!have_w && n.role != RAFT_LEADER) {
+          RS_RC(5);
           w = event_draw(sg, id, t, S);
           have_w = true;
         }
@@ -679,6 +702,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                             emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
                             pold_base, preloc, papplied, elected, mchg, rearm);
       } else if (which < 0) {
+        RS_RC(7);
         if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
           ev = 7;
           // append-entries-rpc (core.clj:56-67): last-entry, then per peer in doseq order
@@ -706,6 +730,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           }
         }
       } else {
+        RS_RC(8);
         ev = type;
         switch (type) {
           case RAFT_MSG_REQUEST_VOTE: {                     // request-vote-handler 91-103
@@ -841,6 +866,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
       RS_PHASE(2);
       if (fault) {                                   // D8: halted with the pre-event state
+        RS_RC(9);
         n.fault = fault;
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
         lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
@@ -854,10 +880,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         if (n.role == RAFT_LEADER) {
           if (!SPEC || ev == 7 || elected) n.deadline = t + S.hb;
         } else if (!SPEC || ev == 6 || rearm || was_leader) {
+          if (!have_w) RS_RC(6);
           if (!have_w) w = event_draw(sg, id, t, S);
           have_w = true;
           n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
         }
+        RS_RC(10);
         n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
         // leader-state words (cold, in HBM)
         if (nm == 1 || nm == 2) {
@@ -894,6 +922,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // {a, b + 1} arriving at t + 1 outside the fault model. A redirect to the node itself
         // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
         if (emit == 4) {
+          RS_RC(11);
           emit = 0;
           if (mb >= S.client_redirects) {
             lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
@@ -919,6 +948,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         RS_PHASE(8);
         // ------------------------------------------------ emission (rpc / respond)
         if (emit) {
+          RS_RC(12);
           bool part = false;
           uint32_t sides = 0;
           if (S.part_ppm) {
@@ -929,6 +959,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
               emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
           if (emit == 3) {
+            RS_RC(13);
             uint32_t* cl =
                 mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
             RS_PHASE(9);
@@ -936,6 +967,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             transmit<N>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
             RS_PHASE(10);
           } else {
+            RS_RC(14);
             RS_PHASE(9);
             // Message words first, for every peer at once: the next-index loads (and then the
             // prev-entry loads) of all peers are independent, so they overlap instead of paying
@@ -995,6 +1027,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     RS_PHASE(3);
     // ---------------------------------------------------------------- P2 network delivery
     if (__ballot(sentmask != 0)) {
+      RS_RC(16);
       // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
       // copy per loop trip in (sender id, copy) order: a single qinsert call site for the wave.
       uint32_t inmask = 0;
@@ -1006,6 +1039,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       if (!active) inmask = 0;
       uint32_t copy = 0;
       while (inmask) {
+        RS_RC(17);
         const int s = __builtin_ctz(inmask);
         const uint2 sr = *reinterpret_cast<const uint2*>(mysrec + s * SRECW);
         uint2 c0 = make_uint2(RAFT_MSG_CLIENT_SET, sr.x), c1 = make_uint2(0, 0),
@@ -1036,6 +1070,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
     const int appended_at = m ? (int)(n.len - m) : -1;
     if (__ballot(m || papplied || (TRACE && tr_cnt))) {
+      RS_RC(19);
       const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
       if (m) {
         const uint32_t pold_len = n.len - m;
@@ -1059,6 +1094,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
       }
       if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
+        RS_RC(21);
         uint32_t cc = S.ccount[sgi];
         uint32_t si = (n.base + n.commit - papplied) % A;
         for (uint32_t i = 0; i < papplied; ++i, ++cc) {
@@ -1086,6 +1122,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // the majority-match scan can raise hwm only when the leader's log reaches past it
     const bool mcheck = (elected || mchg) && n.len > hidx;
     if (__ballot(elected || appended_at >= 0 || mcheck)) {
+      RS_RC(22);
       if (__ballot(elected)) {                       // election safety
         bool bad = false;
 #pragma unroll
@@ -1100,6 +1137,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #else
       if (__ballot(appended_at >= 0)) {              // log matching
 #endif
+        RS_RC(23);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
         bool bad = false;
 #pragma unroll
@@ -1190,6 +1228,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                                   : min(min(n.deadline, n.rq.arr), min(n.rs.arr, cnext));
       const uint32_t E = __ballot(elig && n.rs.c) ? min(wave_min(oth), tend) : t;
       if (E > t + 1 && __ballot(elig && n.rs.arr < E)) {
+        RS_RC(25);
         const uint32_t* qb = qslots(S, sgi, 1);
         const size_t qs = qstride(S, 1);
         for (;;) {
@@ -1211,6 +1250,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
                               (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
           if (__ballot(hbeat || (ev && !simple))) break;   // that tick is the loop's to run
+          RS_RC(26);
           if (ev) {
             QueueR r = n.rs;
             r.h = nh;
@@ -1241,6 +1281,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
     wnext = next_event();
   }
+#ifdef RS_REGIONCOUNT
+  __builtin_amdgcn_wave_barrier();
+  if (lane < RC_WORDS && S.wavelog) S.wavelog[(size_t)wave * 32 + lane] = rcl[lane];
+#endif
 #ifdef RS_WAVELOG
   if (lane == 0 && S.wavelog) {
     const uint64_t wl_end = wall_clock64();
@@ -1344,6 +1388,11 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
 // some phases hold one cluster per tick) a wave is closed early and padded instead of mixing up
 // to ten phases, whose rounds would all be active ticks of the wave (C2: the slowest wave 60 -> 34
 // active ticks for ~5 % more waves, measured offline against the oracle; tick kernel -24 %).
+// The window is 0: a wave holds clusters of one key only. With a one-tick window a wave mixed
+// clusters one tick apart in their heartbeat rounds, so most of its trips ran the heartbeat
+// broadcast and the followers' replies side by side; with one key per wave every trip is one
+// phase of the round (C2: 7.8 -> 6.5 loop trips per wave, 5,724 -> 6,975 waves, tick kernel
+// 0.115 -> 0.093 ms; C3/C4 unchanged).
 //
 // The window is planned per chunk of SCHED_CHUNK buckets, one thread each, restarting at every
 // chunk (16-bucket chunks cost ~1 % more waves than one serial walk); chunk totals are whole
@@ -1354,7 +1403,10 @@ constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 1024, one 
 static_assert(SCHED_CHUNKS == SCHED_PLAN_CHUNKS, "grid bound covers one partial wave per chunk");
 constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
 constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets per block
-constexpr uint32_t SCHED_WINDOW = 1;
+#ifndef RS_SCHED_WINDOW
+#define RS_SCHED_WINDOW 0
+#endif
+constexpr uint32_t SCHED_WINDOW = RS_SCHED_WINDOW;
 static_assert(SCHED_CHUNKS == 1024 && SCHED_KB % SCHED_CHUNK == 0, "one chunk per thread");
 
 template <uint32_t CPW>
