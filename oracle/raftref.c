@@ -44,14 +44,17 @@ static uint32_t ppm(uint32_t w) { return (uint32_t)(((uint64_t)w * 1000000u) >> 
 /* pw_i = (1-p)^(2^i) in 32-bit fixed point, truncating (SIM_SPEC §4 P0). */
 static void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
   pw[0] = ((uint64_t)(1000000u - client_ppm) << 32) / 1000000u;
-  for (int i = 1; i < 32; ++i) pw[i] = (pw[i - 1] * pw[i - 1]) >> 32;
+  for (int i = 1; i < 32; ++i)   /* exact: 2^32 squared (client_ppm = 0) stays 2^32 */
+    pw[i] = pw[i - 1] == 1ull << 32 ? pw[i - 1] : (pw[i - 1] * pw[i - 1]) >> 32;
 }
 
 /* Geometric gap: greedy search for the largest G with (1-p)^G >= (w+1)/2^32. */
 static uint64_t client_gap(uint32_t w, const uint64_t pw[32]) {
   uint64_t u = (uint64_t)w + 1, acc = 1ull << 32, g = 0;
   for (int i = 31; i >= 0; --i) {
-    uint64_t c = (acc * pw[i]) >> 32;
+    /* exact floor(acc * pw_i / 2^32): both factors are <= 2^32 and equal it together only when
+     * client_ppm = 0 (pw_i = 2^32), where the 64-bit product would wrap */
+    uint64_t c = acc == 1ull << 32 ? pw[i] : (acc * pw[i]) >> 32;
     if (c >= u) { acc = c; g += 1ull << i; }
   }
   return g;

@@ -58,7 +58,8 @@ struct DevSim {
   uint32_t* tecount;      // [NN]
   uint32_t TC, TE;
   const unsigned long long* client_pw;  // [32] powers of (1-p) (SIM_SPEC P0); staged into LDS
-  int client_top;                       // highest i with client_pw[i] > 0, -1 if none
+  int client_top;                       // highest i with client_pw[i] > 0, -1 if none,
+                                        // 32 when client_ppm == 0 (every power 2^32)
   unsigned long long* ctr;  // [CTR_COPIES][CTR_STRIDE]: [RAFT_CTR_COUNT] sums, then the first
                             // violation (min) and the largest payload (max); summed by the host
   const uint32_t* perm;     // [slots] wave slot -> cluster or INF (RAFT_SCHED_ALIGNED), null = identity
@@ -128,14 +129,18 @@ __device__ __forceinline__ uint32_t ppm(uint32_t w) { return __umulhi(w, 1000000
 // pw_i = (1-p)^(2^i) in 32-bit fixed point, truncating (SIM_SPEC §4 P0); computed on the host.
 inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
   pw[0] = ((uint64_t)(1000000u - client_ppm) << 32) / 1000000u;
-  for (int i = 1; i < 32; ++i) pw[i] = (pw[i - 1] * pw[i - 1]) >> 32;
+  for (int i = 1; i < 32; ++i)   // exact: 2^32 squared (client_ppm = 0) stays 2^32
+    pw[i] = pw[i - 1] == 1ull << 32 ? pw[i - 1] : (pw[i - 1] * pw[i - 1]) >> 32;
 }
 
 // Geometric gap G(w) of SIM_SPEC §4 P0: the greedy power search over pw[top..0] (higher powers
 // are 0 and never fire). The accumulator starts at 2^32 and every power is below 2^32 when
-// client_ppm > 0 (the only case the gap is drawn for), so after its first step it fits 32 bits
-// and (acc * pw) >> 32 is one v_mul_hi_u32 instead of a 64x64-bit product.
+// client_ppm > 0, so after its first step it fits 32 bits and (acc * pw) >> 32 is one
+// v_mul_hi_u32 instead of a 64x64-bit product.
 __device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
+  // client_ppm == 0 (top == 32; reachable only through a host-written client cursor): every
+  // power is 2^32, so the search takes every step
+  if (top > 31) return 0xFFFFFFFFull;
   const uint64_t u = (uint64_t)w + 1;
   uint32_t acc = 0;
   bool full = true;                 // acc == 2^32

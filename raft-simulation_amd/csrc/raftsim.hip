@@ -169,6 +169,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   d.client_top = -1;
   for (int i = 0; i < 32; ++i)
     if (pw[i]) d.client_top = i;
+  if (pw[0] >> 32) d.client_top = 32;   // client_ppm == 0: every power is 2^32 (rs::client_gap)
   const size_t NN = s->NN;
   d.HB = rs::hot_block_words(s->N);
   if ((rc = dalloc(s, &d.hot, (size_t)s->C * d.HB)) ||

@@ -291,3 +291,21 @@ def test_gpu_step_async_matches_step():
     assert a.counters() == b.counters()
     ms, launches = b.last_step_timing()
     assert launches == 8 and ms > 0
+
+
+@pytest.mark.parametrize("ppm", [0, 30000])
+def test_gpu_host_written_client_cursor(ppm):
+    """A client cursor written by the host (checkpoint/resume through raft_sim_write_clusters) is
+    honoured like any other, also with client_ppm = 0, where every power of the gap search is
+    2^32 and the next injection never comes (SIM_SPEC §4 P0)."""
+    cfg = dict(n_clusters=64, nodes=5, seed=77, client_ppm=ppm, log_cap=64)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    recs = [dict(hwm=(0, 0, 0), client_next=100 + 37 * i, client_count=i) for i in range(64)]
+    g.write_clusters(0, recs)
+    r.write_clusters(0, recs)
+    for _ in range(3):
+        g.step(4000)
+        r.step(4000)
+        assert (g.digest() == r.digest()).all()
+    assert g.counters() == r.counters()
+    assert g.counters()["client_injected"] >= 64

@@ -247,3 +247,16 @@ def test_resume_and_tick_horizon():
         src.step(2)
     with pytest.raises(helpers.RaftSimError):
         src.set_tick(top + 5)
+
+
+def test_client_gap_without_client_rate():
+    """client_ppm = 0 with a host-written cursor (SIM_SPEC §4 P0): that one injection happens, and
+    the gap after it is 2^32 - 1 (never), as the exact integer search gives (pw_i = 2^32)."""
+    cfg = dict(n_clusters=8, nodes=5, seed=77, client_ppm=0, log_cap=64)
+    r = helpers.oracle(**cfg)
+    r.write_clusters(0, [dict(hwm=(0, 0, 0), client_next=100 + i, client_count=i)
+                         for i in range(8)])
+    r.step(5000)
+    assert r.counters()["client_injected"] == 8
+    assert all(c["client_next"] == 0xFFFFFFFF for c in r.read_clusters())
+    assert pyref.client_gap(12345, pyref.client_powers(0)) == 2 ** 32 - 1
