@@ -67,6 +67,8 @@ struct DevSim {
   uint32_t* skey;           // [C] RAFT_SCHED_ALIGNED: cluster's next event - next launch's t0
   uint32_t* shist;          // [SCHED_BUCKETS] histogram of skey (null: schedule fixed)
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
+  uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
+                            // delay: the LITE tick kernel applies
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer

@@ -166,6 +166,8 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   uint64_t pw[32];
   rs::client_powers(cfg->client_ppm, pw);
   d.client_pw = nullptr;
+  d.lite = cfg->client_ppm == 0 && cfg->drop_ppm == 0 && cfg->dup_ppm == 0 && cfg->part_ppm == 0 &&
+           cfg->dmin == cfg->dmax;
   d.client_top = -1;
   for (int i = 0; i < 32; ++i)
     if (pw[i]) d.client_top = i;
@@ -450,6 +452,8 @@ static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t whic
         (i > 0 && in[i].arrival < in[i - 1].arrival))
       return fail(-EINVAL, "invalid message or order");
   }
+  for (uint32_t i = 0; i < count; ++i)   // a queued client-set needs the general kernel (LITE)
+    if ((in[i].hdr & 7) == RAFT_MSG_CLIENT_SET) s->d.lite = 0;
   HIP_OK(hipSetDevice(s->cfg.device));
   const uint32_t gi = cluster * s->N + id - 1;
   std::vector<raft_msg_t> slots(s->Q);
@@ -602,7 +606,10 @@ static int sh_write_clusters(Shard* s, uint32_t c0, uint32_t nc, const raft_clus
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
   std::vector<raft_cluster_t> buf(in, in + nc);
-  for (auto& h : buf) h.reserved[0] = h.reserved[1] = h.reserved[2] = 0;
+  for (auto& h : buf) {
+    h.reserved[0] = h.reserved[1] = h.reserved[2] = 0;
+    if (h.client_next != 0xFFFFFFFFu) s->d.lite = 0;   // a client-set is due: P0 is needed
+  }
   if (nc)
     HIP_OK(hipMemcpy2DAsync(cl_words(s, c0), (size_t)s->d.HB * 4, buf.data(),
                             sizeof(raft_cluster_t), sizeof(raft_cluster_t), nc,

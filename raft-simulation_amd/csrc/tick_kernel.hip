@@ -59,7 +59,7 @@ __device__ __forceinline__ void cell_put(uint32_t* cl, uint4 a, uint4 b) {
 
 // P2 fault draws for one emitted message whose words are already in cell `cl`: the delivery pack
 // (copy delays and count) goes to the cell's last word and the receiver's bit into sentmask.
-template <int N>
+template <int N, bool LITE>
 __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
                                          uint32_t p, bool part, uint32_t sides, uint32_t* cl,
                                          uint32_t& sentmask, uint32_t* lctr) {
@@ -69,7 +69,7 @@ __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t
     return;
   }
   uint32_t pack;
-  if (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax) {
+  if (LITE || (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax)) {
     pack = S.dmin | 1u << 16;
   } else {
     const uint4 w = philox(g, id | P_NET << 8, t, p, S.key0, S.key1);
@@ -130,12 +130,13 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
 // value? Four positions per trip with their eight loads in flight together (a 2000-entry
 // AppendEntries is checked against every peer: one memory round trip per entry was most of C4's
 // time); every slot read is inside the arena, the comparisons past cnt are masked.
+template <int W = 4>
 __device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
                                              uint32_t yi, uint32_t cnt, uint32_t A) {
-  for (uint32_t i = 0; i < cnt; i += 4) {
-    uint2 x[4], y[4];
+  for (uint32_t i = 0; i < cnt; i += W) {
+    uint2 x[W], y[W];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < W; ++j) {
       x[j] = xa[xi];
       y[j] = ya[yi];
       xi = xi + 1 == A ? 0 : xi + 1;
@@ -143,7 +144,7 @@ __device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const
     }
     bool c = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c |= i + j < cnt && x[j].x == y[j].x && x[j].y != y[j].y;
+    for (int j = 0; j < W; ++j) c |= i + j < cnt && x[j].x == y[j].x && x[j].y != y[j].y;
     if (c) return true;
   }
   return false;
@@ -157,9 +158,9 @@ __device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const
 #ifndef RS_COPY_BATCH
 #define RS_COPY_BATCH 4
 #endif
+template <uint32_t B = RS_COPY_BATCH>
 __device__ __forceinline__ void arena_copy(uint2* dst, uint32_t di, const uint2* src, uint32_t si,
                                            uint32_t cnt, uint32_t A) {
-  constexpr uint32_t B = RS_COPY_BATCH;
   uint32_t i = 0;
   if (A >= B) {
     for (; i + B <= cnt; i += B) {
@@ -421,9 +422,14 @@ __device__ __forceinline__ uint32_t sched_bucket(uint32_t ev, uint32_t t0) {
   return d < SCHED_BUCKETS - 1 ? (uint32_t)d : SCHED_BUCKETS - 1;
 }
 
-template <int N, bool TRACE, bool SPEC>
+// LITE: the launch has no client traffic, no faults and a fixed delay (DevSim::lite, set by the
+// host; C2): P0, client-set handling and redirects cannot occur, every emission takes the
+// fault-free delivery pack, and P3/P4 copy and compare one entry per memory round trip (they only
+// see host-written logs there). The compiler then drops that code: 121 -> ~100 VGPRs at N = 5.
+template <int N, bool TRACE, bool SPEC, bool LITE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+  static_assert(!LITE || (!TRACE && !SPEC), "LITE is the plain faithful kernel");
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
@@ -497,7 +503,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   // recomputed after every tick that did work. Idle ticks then cost one scalar compare.
   auto next_event = [&]() {
     const uint32_t m = n.fault ? INF : min(n.deadline, min(n.rq.arr, n.rs.arr));
-    return wave_min(active ? min(m, cnext) : INF);
+    return wave_min(active ? (LITE ? m : min(m, cnext)) : INF);
   };
   uint32_t wnext = next_event();
 #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
@@ -563,11 +569,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // ---------------------------------------------------------- P0 client injection (D9, D14)
     bool inj = false;
     uint32_t injv = 0;
-    const bool cinj = active && t == cnext;
+    const bool cinj = !LITE && active && t == cnext;
 #ifdef RS_WAVELOG
     wl_inj += __ballot(cinj) ? 1 : 0;
 #endif
-    if (__ballot(cinj)) {
+    if (!LITE && __ballot(cinj)) {
       RS_RC(1);
       if (cinj) {
         const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
@@ -585,7 +591,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // kept in registers (dcs) instead of a global store + same-tick load; it is written to the
     // queue only if this tick's alts!! choice takes the RES queue instead.
     bool dcs = false;
-    if (__ballot(inj)) {
+    if (!LITE && __ballot(inj)) {
       if (inj) {
         if (live && n.rq.c == 0) dcs = true;
         else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
@@ -795,6 +801,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             break;
           }
           case RAFT_MSG_CLIENT_SET: {                        // client-set-handler 151-160
+            if (LITE) break;                                 // (no client traffic)
             if (n.role != RAFT_LEADER) {                     // redirect-client: no state change
               emit = 4;
               break;
@@ -921,7 +928,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
         // {a, b + 1} arriving at t + 1 outside the fault model. A redirect to the node itself
         // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
-        if (emit == 4) {
+        if (!LITE && emit == 4) {
           RS_RC(11);
           emit = 0;
           if (mb >= S.client_redirects) {
@@ -951,7 +958,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           RS_RC(12);
           bool part = false;
           uint32_t sides = 0;
-          if (S.part_ppm) {
+          if (!LITE && S.part_ppm) {
             const uint4 pw = philox(sg, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
             part = ppm(pw.x) < S.part_ppm;
             sides = pw.y;
@@ -964,7 +971,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                 mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
             RS_PHASE(9);
             cell_put(cl, ra, rb);
-            transmit<N>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
+            transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
             RS_PHASE(10);
           } else {
             RS_RC(14);
@@ -1014,7 +1021,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
-              transmit<N>(S, sg, t, id, p, part, sides,
+              transmit<N, LITE>(S, sg, t, id, p, part, sides,
                           mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, sentmask,
                           lctr);
             }
@@ -1075,7 +1082,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       if (m) {
         const uint32_t pold_len = n.len - m;
         // physical slots advance with a wrap instead of a per-entry modulo
-        if (preloc) arena_copy(sar, n.base % A, sar, pold_base % A, pold_len, A);
+        if (preloc)
+          arena_copy<LITE ? 1 : RS_COPY_BATCH>(sar, n.base % A, sar, pold_base % A, pold_len, A);
         uint32_t di = (n.base + pold_len) % A;
         if (pkind == PLAN_ENTRY) {
           sar[di] = make_uint2(ppoff, ppcnt);
@@ -1089,7 +1097,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             sar[di] = make_uint2(0, 0);
             di = di + 1 == A ? 0 : di + 1;
           }
-          arena_copy(sar, di, sa, si, m - evicted, A);
+          arena_copy<LITE ? 1 : RS_COPY_BATCH>(sar, di, sa, si, m - evicted, A);
           lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
         }
       }
@@ -1147,7 +1155,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             const uint2* oa = arena_of(S, sgi - k + s);
             const uint32_t hi = n.len < sl ? n.len : sl, lo = (uint32_t)appended_at;
             if (hi > lo)
-              bad = log_conflict(sar, (n.base + lo) % A, oa, (sb + lo) % A, hi - lo, A);
+              bad = log_conflict<LITE ? 1 : 4>(sar, (n.base + lo) % A, oa, (sb + lo) % A, hi - lo, A);
           }
         }
         if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
@@ -1219,7 +1227,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // Only where it pays: clusters of up to five nodes without client traffic (C2; with client
     // traffic the wave has an event nearly every tick, measured C3 +3 %), and it would cost the
     // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
-    if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (!S.client_ppm) {
+    if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (LITE || !S.client_ppm) {
       // leaders whose responses can drain: a log past the hwm makes a success response a
       // checker event (C3/C4 replication), so those leaders stay with the loop
       const bool elig = active && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
@@ -1646,11 +1654,14 @@ void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, h
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = S.perm ? sched_slots_bound(S.C, N) / CPW : (S.C + CPW - 1) / CPW;
   if (S.TC)
-    hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC>), dim3(waves), dim3(64), lds, st, ev0, ev1,
-                          0, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC, false>), dim3(waves), dim3(64), lds, st, ev0,
+                          ev1, 0, S, t0, nt);
+  else if (!SPEC && S.lite)
+    hipExtLaunchKernelGGL((tick_kernel<N, false, false, true>), dim3(waves), dim3(64), lds, st, ev0,
+                          ev1, 0, S, t0, nt);
   else
-    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC>), dim3(waves), dim3(64), lds, st, ev0, ev1,
-                          0, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false>), dim3(waves), dim3(64), lds, st,
+                          ev0, ev1, 0, S, t0, nt);
 }
 
 template <int N>
@@ -1676,9 +1687,9 @@ hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st
   }
 }
 
-template <int N, bool TRACE, bool SPEC>
+template <int N, bool TRACE, bool SPEC, bool LITE = false>
 hipError_t configure_one() {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC>),
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC, LITE>),
                              hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)block_lds_bytes<N, SPEC>());
 }
@@ -1687,7 +1698,8 @@ template <int N>
 hipError_t configure_n() {
   hipError_t e = hipSuccess;
   if ((e = configure_one<N, false, false>()) || (e = configure_one<N, true, false>()) ||
-      (e = configure_one<N, false, true>()) || (e = configure_one<N, true, true>()))
+      (e = configure_one<N, false, true>()) || (e = configure_one<N, true, true>()) ||
+      (e = configure_one<N, false, false, true>()))
     return e;
   return hipSuccess;
 }
