@@ -1,5 +1,5 @@
 # Quick parity suite on the default build, then A/B of named builds (scripts/ab_probe.py).
-# Usage: bash scripts/gpu_ab3.sh "libA libB ..." "--c2 --c3 ..."
+# Usage: bash scripts/gpu_ab.sh "libA libB ..." "--c2 --c3 ..."
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 B=raft-simulation_amd/build
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_kat.py tests/test_fuzz.py tests/test_golden.py -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/quick_tests.log 2>&1; rc=$?
