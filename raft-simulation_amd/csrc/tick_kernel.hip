@@ -63,7 +63,7 @@ template <int N, bool LITE>
 __device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
                                          uint32_t p, bool part, uint32_t sides, uint32_t* cl,
                                          uint32_t& sentmask, uint32_t* lctr) {
-  lctr_add(lctr, RAFT_CTR_SENT, 1);
+  // RAFT_CTR_SENT is counted by the caller (once per emission: 1 or N - 1)
   if (part && (((sides >> id) ^ (sides >> p)) & 1)) {
     lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
     return;
@@ -971,6 +971,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                 mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
             RS_PHASE(9);
             cell_put(cl, ra, rb);
+            lctr_add(lctr, RAFT_CTR_SENT, 1);
             transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
             RS_PHASE(10);
           } else {
@@ -1018,6 +1019,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             }
             RS_PHASE(11);
             if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
+            lctr_add(lctr, RAFT_CTR_SENT, N - 1);
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -1391,30 +1393,24 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   atomicAdd(&S.shist[key], 1u);
 }
 
-// Window-limited packing. Clusters are taken in key order, but a wave never holds keys more than
-// SCHED_WINDOW ticks apart: where the keys are sparse (the first elections bunch near el_base, so
-// some phases hold one cluster per tick) a wave is closed early and padded instead of mixing up
-// to ten phases, whose rounds would all be active ticks of the wave (C2: the slowest wave 60 -> 34
-// active ticks for ~5 % more waves, measured offline against the oracle; tick kernel -24 %).
-// The window is 0: a wave holds clusters of one key only. With a one-tick window a wave mixed
-// clusters one tick apart in their heartbeat rounds, so most of its trips ran the heartbeat
-// broadcast and the followers' replies side by side; with one key per wave every trip is one
-// phase of the round (C2: 7.8 -> 6.5 loop trips per wave, 5,724 -> 6,975 waves, tick kernel
-// 0.115 -> 0.093 ms; C3/C4 unchanged).
+// Key-pure packing. A wave is active on the union of its clusters' event ticks, so a wave holds
+// one key (a zero-tick window): clusters one tick apart in their heartbeat rounds would run the
+// heartbeat broadcast and the followers' replies on the same trips, each trip paying for both
+// branches. Measured on C2 (tick kernel per 10k-tick launch): one-tick window (most waves straddle
+// two keys) 0.115 ms; one key per wave 0.093 ms for 22 % more waves; one key per wave except
+// that the remainders of two adjacent keys share a wave (13 % fewer waves, 6 % fewer wave trips)
+// 0.099 ms -- a mixed trip costs about two pure ones. Wider windows mixed up to ten phases per
+// wave (the slowest C2 wave 60 active ticks).
 //
-// The window is planned per chunk of SCHED_CHUNK buckets, one thread each, restarting at every
-// chunk (16-bucket chunks cost ~1 % more waves than one serial walk); chunk totals are whole
-// waves. If the padded plan would exceed the grid bound (sched_slots_bound), every chunk falls
-// back to the plain counting sort.
+// The plan is made per chunk of SCHED_CHUNK buckets, one thread each, restarting at every chunk;
+// chunk totals are whole waves. If the padded plan would exceed the grid bound
+// (sched_slots_bound), every chunk falls back to the plain counting sort.
 constexpr uint32_t SCHED_CHUNK = 16;
 constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 1024, one per thread
 static_assert(SCHED_CHUNKS == SCHED_PLAN_CHUNKS, "grid bound covers one partial wave per chunk");
 constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
 constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets per block
-#ifndef RS_SCHED_WINDOW
-#define RS_SCHED_WINDOW 0
-#endif
-constexpr uint32_t SCHED_WINDOW = RS_SCHED_WINDOW;
+constexpr uint32_t SCHED_WINDOW = 0;
 static_assert(SCHED_CHUNKS == 1024 && SCHED_KB % SCHED_CHUNK == 0, "one chunk per thread");
 
 template <uint32_t CPW>
