@@ -499,13 +499,21 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
 
-  // Earliest tick at which any lane of the wave can have an event (deadline or queue head);
-  // recomputed after every tick that did work. Idle ticks then cost one scalar compare.
+  // Per-cluster reductions over the cluster's N lanes (every lane of the wave must be active).
+  const uint32_t cmask = (1u << N) - 1;
+  auto cluster_min = [&](uint32_t x) {
+    uint32_t m = x;
+#pragma unroll
+    for (int s = 0; s < N; ++s) m = min(m, (uint32_t)__shfl(x, bl0 + s));
+    return m;
+  };
+  auto cluster_any = [&](bool x) { return ((uint32_t)(__ballot(x) >> bl0) & cmask) != 0; };
+  // Earliest tick at which any node of the lane's cluster can have an event (deadline, queue head
+  // or the next client-set), the same for all the cluster's lanes.
   auto next_event = [&]() {
     const uint32_t m = n.fault ? INF : min(n.deadline, min(n.rq.arr, n.rs.arr));
-    return wave_min(active ? (LITE ? m : min(m, cnext)) : INF);
+    return cluster_min(active ? (LITE ? m : min(m, cnext)) : INF);
   };
-  uint32_t wnext = next_event();
 #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
   const uint64_t wl_start = wall_clock64();
   uint32_t wl_active = 0, wl_first = INF, wl_drain = 0, wl_inj = 0, wl_dead = 0;
@@ -536,17 +544,23 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #endif
 
   const uint32_t tend = t0 + nt;
-  for (uint32_t t = t0;; ++t) {
-    // Ticks before the wave's next event change nothing (every handler, injection and delivery
-    // is keyed to a deadline, a queue head or the injection cursor, all folded into wnext), so
-    // the wave jumps over them: discrete-event skipping with tick-exact results.
-    if (t < wnext) t = wnext < tend ? wnext : tend;
-    if (t == tend) break;
+  // Every cluster keeps its own clock. Ticks before a cluster's next event change nothing for it
+  // (every handler, injection and delivery is keyed to a deadline, a queue head or the injection
+  // cursor), and clusters never interact, so each trip of the loop runs every cluster's next
+  // event tick -- not the wave's: a wave makes as many trips as its busiest cluster has event
+  // ticks, instead of the union of its clusters' event ticks (discrete-event skipping per
+  // cluster, tick-exact; Philox draws are keyed by the cluster's own tick).
+  uint32_t tnext = t0;                      // the cluster's first tick not yet simulated
+  for (;;) {
+    uint32_t t = max(tnext, next_event());
+    t = t < tend ? t : tend;
+    const bool on = active && t < tend;     // the cluster has a tick to run in this trip
+    if (!__ballot(on)) break;
     RS_RC(0);
 #ifdef RS_WAVELOG
     wl_ts = __builtin_amdgcn_s_memtime();
 #endif
-    const bool live = active && !n.fault;
+    const bool live = on && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
     // address and shuffle index the active-tick phases use out of the tick loop, where each would
     // hold a VGPR across all ticks (~50 VGPRs in all); recomputing them costs a few VALU per
@@ -569,7 +583,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // ---------------------------------------------------------- P0 client injection (D9, D14)
     bool inj = false;
     uint32_t injv = 0;
-    const bool cinj = !LITE && active && t == cnext;
+    const bool cinj = !LITE && on && t == cnext;
 #ifdef RS_WAVELOG
     wl_inj += __ballot(cinj) ? 1 : 0;
 #endif
@@ -1045,7 +1059,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         const uint32_t sm = __shfl(sentmask, bl + s);
         inmask |= ((sm >> id) & 1u) << s;
       }
-      if (!active) inmask = 0;
+      if (!on) inmask = 0;
       uint32_t copy = 0;
       while (inmask) {
         RS_RC(17);
@@ -1172,7 +1186,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
       }
       int32_t cm = -1;
       uint32_t ct = 0, cv = 0;
-      if (active && n.role == RAFT_LEADER && mcheck) {
+      if (on && n.role == RAFT_LEADER && mcheck) {
         int32_t vals[N];
         vals[0] = (int32_t)n.len;
         int j = 1;
@@ -1207,7 +1221,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           const uint32_t st = __shfl(ct, bl + s), sv = __shfl(cv, bl + s);
           if (sm > best) { best = sm; bt = st; bv = sv; }
         }
-        if (active && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
+        if (on && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
       }
     }
     RS_PHASE(6);
@@ -1219,77 +1233,87 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // ------------------------------------------------------- append-response drain (faithful)
     // A leader answers each append-response with no message, no log write and -- while its log
     // does not reach past the checker's high-water mark -- no check: the event touches its own
-    // words only (core.clj:141-149, timer 171-174). Ticks at which the wave's only events are
+    // words only (core.clj:141-149, timer 171-174). Ticks at which a cluster's only events are
     // such responses are therefore run here without P0 and P2-P4, one response per leader per
-    // tick as above, until the wave's next other event E (the REQ head and client-set of every
-    // lane, and the deadline and RES head of every lane that is not a live leader). A tick at
+    // tick as above, until the cluster's next other event E (the REQ head and client-set of every
+    // node, and the deadline and RES head of every node that is not a live leader). A tick at
     // which a leader's event is anything else (a heartbeat, or a head message that is not such
-    // a response) ends the drain before that tick; the loop above then runs it. Steady state: a
-    // heartbeat round's four responses at the leader take one trip through here, not four ticks.
+    // a response) ends the cluster's drain before that tick; the loop above then runs it. Steady
+    // state: a heartbeat round's four responses at the leader take one trip through here, not four ticks.
     // Only where it pays: clusters of up to five nodes without client traffic (C2; with client
     // traffic the wave has an event nearly every tick, measured C3 +3 %), and it would cost the
     // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
     if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (LITE || !S.client_ppm) {
       // leaders whose responses can drain: a log past the hwm makes a success response a
       // checker event (C3/C4 replication), so those leaders stay with the loop
-      const bool elig = active && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
-      const uint32_t oth = (!active || n.fault) ? INF
-                           : elig ? min(n.rq.arr, cnext)
-                                  : min(min(n.deadline, n.rq.arr), min(n.rs.arr, cnext));
-      const uint32_t E = __ballot(elig && n.rs.c) ? min(wave_min(oth), tend) : t;
-      if (E > t + 1 && __ballot(elig && n.rs.arr < E)) {
-        RS_RC(25);
-        const uint32_t* qb = qslots(S, sgi, 1);
-        const size_t qs = qstride(S, 1);
-        for (;;) {
-          const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
-          const uint32_t tau = max(wave_min(nxt), t + 1);
-          if (tau >= E) break;
-          const bool ev = elig && n.rs.arr <= tau;          // a ready message beats the timer
-          const bool hbeat = elig && !ev && n.deadline <= tau;
-          uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
-          uint32_t narr = INF;
-          const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
-          if (ev) {
-            const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
-            m0 = sp[0];
-            m1 = sp[1];
-            if (n.rs.c > 1) narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
-          }
-          const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
-          const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
-                              (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
-          if (__ballot(hbeat || (ev && !simple))) break;   // that tick is the loop's to run
-          RS_RC(26);
-          if (ev) {
-            QueueR r = n.rs;
-            r.h = nh;
-            r.c -= 1;
-            r.arr = r.c ? narr : INF;
-            r.tail = r.c ? r.tail : 0u;
-            if (!r.c) r.h = 0;
-            n.rs = r;
-            if (flag) {                                  // append-response-handler 145-149
-              n.lsp = 1;
-              n.keys |= 1u << src;
-              lsw.next(src - 1) = (int32_t)m1.x;
-              lsw.match(src - 1) = (int32_t)m0.w;
-            } else {                                     // 143-144: (dec next-index)
-              lsw.next(src - 1) -= 1;
+      const bool elig = on && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
+      if (__ballot(elig && n.rs.c)) {
+        const uint32_t oth = (!on || n.fault) ? INF
+                             : elig ? min(n.rq.arr, cnext)
+                                    : min(min(n.deadline, n.rq.arr), min(n.rs.arr, cnext));
+        // the cluster's next other event E; a cluster drains while its leaders' responses are
+        // its only events before E
+        const uint32_t E = min(cluster_min(oth), tend);
+        const bool any_res = cluster_any(elig && n.rs.c);
+        const bool any_ready = cluster_any(elig && n.rs.arr < E);
+        bool dr = on && any_res && any_ready && E > t + 1;
+        if (__ballot(dr)) {
+          RS_RC(25);
+          const uint32_t* qb = qslots(S, sgi, 1);
+          const size_t qs = qstride(S, 1);
+          for (;;) {
+            const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
+            const uint32_t tau = max(cluster_min(nxt), t + 1);
+            dr = dr && tau < E;
+            const bool ev = dr && elig && n.rs.arr <= tau;  // a ready message beats the timer
+            const bool hbeat = dr && elig && !ev && n.deadline <= tau;
+            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
+            uint32_t narr = INF;
+            const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
+            if (ev) {
+              const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
+              m0 = sp[0];
+              m1 = sp[1];
+              if (n.rs.c > 1)
+                narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
             }
-            n.deadline = tau + S.hb;
-            n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
-                                  n.term, 0);
-            lctr_add(lctr, RAFT_CTR_EV_AR, 1);
-          }
-          t = tau;
+            const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
+            const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
+                                (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
+            // a tick at which any node of the cluster needs the loop above is the loop's to run
+            dr = dr && !cluster_any(hbeat || (ev && !simple));
+            if (!__ballot(dr)) break;
+            RS_RC(26);
+            if (dr && ev) {
+              QueueR r = n.rs;
+              r.h = nh;
+              r.c -= 1;
+              r.arr = r.c ? narr : INF;
+              r.tail = r.c ? r.tail : 0u;
+              if (!r.c) r.h = 0;
+              n.rs = r;
+              if (flag) {                                  // append-response-handler 145-149
+                n.lsp = 1;
+                n.keys |= 1u << src;
+                lsw.next(src - 1) = (int32_t)m1.x;
+                lsw.match(src - 1) = (int32_t)m0.w;
+              } else {                                     // 143-144: (dec next-index)
+                lsw.next(src - 1) -= 1;
+              }
+              n.deadline = tau + S.hb;
+              n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
+                                    n.term, 0);
+              lctr_add(lctr, RAFT_CTR_EV_AR, 1);
+            }
+            if (dr) t = tau;
 #ifdef RS_WAVELOG
-          ++wl_drain;
+            ++wl_drain;
 #endif
+          }
         }
       }
     }
-    wnext = next_event();
+    tnext = t + 1;
   }
 #ifdef RS_REGIONCOUNT
   __builtin_amdgcn_wave_barrier();
