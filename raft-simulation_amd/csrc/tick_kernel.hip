@@ -384,10 +384,12 @@ constexpr int RC_WORDS = 32;
 #else
 constexpr int RC_WORDS = 0;
 #endif
+// TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key)
+constexpr int TRIP_WORDS = 64;
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
-         RC_WORDS;
+         TRIP_WORDS + RC_WORDS;
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -400,6 +402,9 @@ constexpr size_t block_lds_bytes() {
 // ends (measured: 4-wave workgroups 1-2 % slower on C2/C3/C4).
 #ifndef RS_MIN_WAVES_PER_EU
 #define RS_MIN_WAVES_PER_EU 1
+#endif
+#ifndef RS_PACK_ACTIVITY   // 0: client-traffic launches packed by next event too (A/B builds)
+#define RS_PACK_ACTIVITY 1
 #endif
 #ifndef RS_DRAIN   // 0: no append-response drain (A/B builds)
 #define RS_DRAIN 1
@@ -443,9 +448,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+  uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
+  tripsL[lane] = 0;          // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
 #ifdef RS_REGIONCOUNT
   // region i executed by the wave (any lane active): the first active lane counts it
-  uint32_t* rcl = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
+  uint32_t* rcl = tripsL + TRIP_WORDS;
   if (lane < RC_WORDS) rcl[lane] = 0;
 #define RS_RC(i)                                                       \
   do {                                                                 \
@@ -556,6 +563,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     t = t < tend ? t : tend;
     const bool on = active && t < tend;     // the cluster has a tick to run in this trip
     if (!__ballot(on)) break;
+    if (!LITE && S.client_ppm) tripsL[lane] += on;
     RS_RC(0);
 #ifdef RS_WAVELOG
     wl_ts = __builtin_amdgcn_s_memtime();
@@ -1241,7 +1249,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // a response) ends the cluster's drain before that tick; the loop above then runs it. Steady
     // state: a heartbeat round's four responses at the leader take one trip through here, not four ticks.
     // Only where it pays: clusters of up to five nodes without client traffic (C2; with client
-    // traffic the wave has an event nearly every tick, measured C3 +3 %), and it would cost the
+    // traffic a cluster has an event nearly every tick of a burst: measured C3 +3 % with one
+    // wave-wide clock, unchanged with per-cluster clocks, C4-N9 +1 %), and it would cost the
     // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
     if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (LITE || !S.client_ppm) {
       // leaders whose responses can drain: a log past the hwm makes a success response a
@@ -1345,7 +1354,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #pragma unroll
     for (int s = 0; s < N; ++s) cm = min(cm, (uint32_t)__shfl(me, bl0 + s));
     const bool head = active && k0 == 0;
-    const uint32_t key = head ? sched_bucket(cm, tend) : INF;
+    // With client traffic every cluster is busy on most ticks of a burst and a wave lasts as
+    // long as its busiest cluster (per-cluster clocks): clusters are then packed by how many
+    // event ticks they ran in this launch, busiest first (they start first and are done before
+    // the tail), instead of by their next event.
+    const uint32_t key = !head ? INF
+                         : RS_PACK_ACTIVITY && S.client_ppm
+                             ? SCHED_BUCKETS - 1 - min(tripsL[lane], SCHED_BUCKETS - 1)
+                             : sched_bucket(cm, tend);
     if (head) S.skey[c] = key;
     // a packed wave's clusters usually share their next key: one histogram atomic for the wave
     const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
