@@ -1433,14 +1433,17 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
   atomicAdd(&S.shist[key], 1u);
 }
 
-// Key-pure packing. A wave is active on the union of its clusters' event ticks, so a wave holds
-// one key (a zero-tick window): clusters one tick apart in their heartbeat rounds would run the
-// heartbeat broadcast and the followers' replies on the same trips, each trip paying for both
-// branches. Measured on C2 (tick kernel per 10k-tick launch): one-tick window (most waves straddle
-// two keys) 0.115 ms; one key per wave 0.093 ms for 22 % more waves; one key per wave except
-// that the remainders of two adjacent keys share a wave (13 % fewer waves, 6 % fewer wave trips)
-// 0.099 ms -- a mixed trip costs about two pure ones. Wider windows mixed up to ten phases per
-// wave (the slowest C2 wave 60 active ticks).
+// Packing keys in order. Launches with client traffic pack by activity (the tick kernel's key:
+// event ticks run in the previous launch) and keep waves key-pure (a zero-tick window, padded
+// slots): a wave lasts as long as its busiest cluster. Launches without client traffic (C2) pack
+// by next event tick with no padding: with per-cluster clocks, clusters whose heartbeat rounds are
+// a few ticks apart still run the same phase on the same trips (each on its own tick), so a wave
+// needs similar keys, not equal ones. Measured (C2 tick kernel per launch): with one wave-wide
+// clock a one-tick window cost 0.115 ms against 0.093 key-pure (most waves straddled two keys and
+// ran the broadcast and the replies side by side); with per-cluster clocks key-pure 0.094 ms,
+// one-tick window 0.087, unpadded 0.087 (fewest waves). C3 with activity keys: unpadded -1.6 %,
+// C4-N9 +3.8 %: key-pure kept there. Wider windows under one wave-wide clock mixed up to ten
+// phases per wave (the slowest C2 wave 60 active ticks).
 //
 // The plan is made per chunk of SCHED_CHUNK buckets, one thread each, restarting at every chunk;
 // chunk totals are whole waves. If the padded plan would exceed the grid bound
@@ -1496,7 +1499,8 @@ __global__ void __launch_bounds__(1024) sched_range_kernel(DevSim S, uint32_t* z
     const uint4 v = h4[i];
     cnt[4 * i] = v.x; cnt[4 * i + 1] = v.y; cnt[4 * i + 2] = v.z; cnt[4 * i + 3] = v.w;
   }
-  uint32_t tot = plan_chunk<CPW>(cnt, st, true);
+  // client traffic (activity keys): key-pure waves; otherwise keys in order without padding
+  uint32_t tot = plan_chunk<CPW>(cnt, st, S.client_ppm != 0);
   // exclusive scan of the chunk totals: wave scan, then the 16 wave totals
   uint32_t inc = tot;
 #pragma unroll
