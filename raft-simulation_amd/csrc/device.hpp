@@ -23,8 +23,10 @@
 
 namespace rs {
 
+// 1: each Philox round takes both halves of its two 32x32-bit products from one v_mad_u64_u32
+// each instead of a mul_lo + mul_hi pair (measured C4-N9 -5.5 %, C3 -1.6 %, C2 unchanged)
 #ifndef RS_PHILOX_MAD
-#define RS_PHILOX_MAD 0
+#define RS_PHILOX_MAD 1
 #endif
 
 constexpr uint32_t INF = 0xFFFFFFFFu;
