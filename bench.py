@@ -197,8 +197,9 @@ def run_workload(name, args, world, rank, local_rank, dist):
                      "bytes_per_launch": event_bytes, "avg_launch_ms": avg_launch_ms,
                      "launches": launches, "ticks_per_launch": ticks_per_launch,
                      "kernel_src_sha": kernel_build_hash(),
-                     "limiter": "latency of the active ticks' dependent instruction and memory "
-                                "chains (DESIGN.md), not HBM bandwidth",
+                     "limiter": "issue of the active trips' divergent instruction stream "
+                                "(PMC instruction counts, region counts: DESIGN.md), not HBM "
+                                "bandwidth",
                      "per_tick_model": {"bytes_per_node_tick": per_tick_b,
                                         "achieved": per_tick_gbs,
                                         "note": "SURVEY 8(d) B(N) charged to every node-tick "
