@@ -1451,8 +1451,14 @@ __global__ void sched_key_kernel(DevSim S, uint32_t t0) {
 constexpr uint32_t SCHED_CHUNK = 16;
 constexpr uint32_t SCHED_CHUNKS = SCHED_BUCKETS / SCHED_CHUNK;     // 1024, one per thread
 static_assert(SCHED_CHUNKS == SCHED_PLAN_CHUNKS, "grid bound covers one partial wave per chunk");
-constexpr uint32_t SCHED_RANGE_BLOCKS = 64;
-constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 256 buckets per block
+// Workgroups of the schedule kernel, each owning SCHED_KB buckets. Measured per rebuild (C2 65,536
+// / C3 1M clusters): 16 blocks 27.4 us / -, 64: 14.5 / 443 us, 256: 11.3 / 402 us, 512: 16.6 /
+// 322 us, 1024: 28.5 / 337 us (every block reads all keys; fewer buckets per block place faster).
+#ifndef RS_SCHED_BLOCKS
+#define RS_SCHED_BLOCKS 256
+#endif
+constexpr uint32_t SCHED_RANGE_BLOCKS = RS_SCHED_BLOCKS;
+constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 64 buckets per block
 constexpr uint32_t SCHED_WINDOW = 0;
 static_assert(SCHED_CHUNKS == 1024 && SCHED_KB % SCHED_CHUNK == 0, "one chunk per thread");
 
