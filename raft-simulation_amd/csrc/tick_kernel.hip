@@ -1483,7 +1483,7 @@ __device__ uint32_t plan_chunk(const uint32_t (&cnt)[SCHED_CHUNK], uint32_t (&st
 }
 
 // One launch: every block plans all chunks from the histogram (L2-resident, 64 KiB), scans the
-// chunk totals, and places the clusters of its own 256-bucket range at their bucket's slot plus
+// chunk totals, and places the clusters of its own SCHED_KB-bucket range at their bucket's slot plus
 // their rank (LDS atomics, no global ones). It first marks its slots empty (padding reads INF).
 // Each block reads all keys (L2-resident, 4 B per cluster). The histogram is double-buffered: this
 // kernel reads S.shist and zeroes `zero`, which the next tick launch fills (the host swaps the
