@@ -1270,6 +1270,54 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           RS_RC(25);
           const uint32_t* qb = qslots(S, sgi, 1);
           const size_t qs = qstride(S, 1);
+          // A cluster with one eligible leader (the usual case) drains in that lane alone: its
+          // ticks are the leader's own, so the loop needs no cluster reductions per tick. The
+          // stop rules are the cluster loop's below: tau reaches E, a heartbeat falls due, or the
+          // head message is not such a response.
+          const uint32_t em = (uint32_t)(__ballot(elig) >> bl0) & cmask;
+          const bool solo = dr && __popc(em) == 1;
+          if (__ballot(solo)) {
+            if (solo && elig) {
+              for (;;) {
+                const uint32_t tau = max(min(n.rs.arr, n.deadline), t + 1);
+                if (tau >= E || n.rs.arr > tau) break;       // E, or the heartbeat's tick
+                const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
+                const uint4 m0 = sp[0], m1 = sp[1];
+                const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
+                uint32_t narr = INF;
+                if (n.rs.c > 1)
+                  narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
+                const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15,
+                               flag = (hdr >> 7) & 1;
+                if (!((hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
+                      (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1))))
+                  break;
+                QueueR r = n.rs;
+                r.h = nh;
+                r.c -= 1;
+                r.arr = r.c ? narr : INF;
+                r.tail = r.c ? r.tail : 0u;
+                if (!r.c) r.h = 0;
+                n.rs = r;
+                if (flag) {                                // append-response-handler 145-149
+                  n.lsp = 1;
+                  n.keys |= 1u << src;
+                  lsw.next(src - 1) = (int32_t)m1.x;
+                  lsw.match(src - 1) = (int32_t)m0.w;
+                } else {                                   // 143-144: (dec next-index)
+                  lsw.next(src - 1) -= 1;
+                }
+                n.deadline = tau + S.hb;
+                n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
+                                      n.term, 0);
+                lctr_add(lctr, RAFT_CTR_EV_AR, 1);
+                t = tau;
+              }
+            }
+            const uint32_t lt = __shfl(t, bl0 + (em ? (int)__builtin_ctz(em) : 0));
+            if (solo) t = lt;                              // the cluster takes the leader's clock
+            dr = dr && !solo;
+          }
           for (;;) {
             const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
             const uint32_t tau = max(cluster_min(nxt), t + 1);
