@@ -1042,12 +1042,19 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             RS_PHASE(11);
             if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
             lctr_add(lctr, RAFT_CTR_SENT, N - 1);
+            if constexpr (LITE) {          // every peer gets one copy after the fixed delay
+#pragma unroll
+              for (int j = 0; j < N - 1; ++j)
+                mycells[(k * (N - 1) + j) * CELLW + CELLW - 1] = S.dmin | 1u << 16;
+              sentmask |= peers;
+            } else {
 #pragma unroll 1
-            for (int p = 1; p <= N; ++p) {
-              if (p == (int)id) continue;
-              transmit<N, LITE>(S, sg, t, id, p, part, sides,
-                          mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, sentmask,
-                          lctr);
+              for (int p = 1; p <= N; ++p) {
+                if (p == (int)id) continue;
+                transmit<N, LITE>(S, sg, t, id, p, part, sides,
+                            mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW,
+                            sentmask, lctr);
+              }
             }
             RS_PHASE(10);
           }
@@ -1080,7 +1087,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
           c0 = cl[0]; c1 = cl[1]; c2 = cl[2];
         }
-        const uint32_t d = copy == 0 ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
+        const uint32_t d = (LITE || copy == 0) ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
         const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
         QueueR q = which ? n.rs : n.rq;
         const uint4 q0 = make_uint4(t + d, c0.x, s != k ? sr.x : 0u, sr.y),
@@ -1088,7 +1095,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
         if (which) n.rs = q;
         else n.rq = q;
-        if (++copy >= (c2.y >> 16)) {
+        if (LITE || ++copy >= (c2.y >> 16)) {   // LITE: one copy per message
           copy = 0;
           inmask &= inmask - 1;
         }
