@@ -36,12 +36,14 @@ constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min v
 constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
 static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
-constexpr int PW_WORDS = 64;
+constexpr int PW_WORDS = 64;    // 32 x u64 client-gap powers at the start of the block's LDS
 // Waves flush their counters into one of CTR_COPIES copies of the counter block (wave index mod
 // CTR_COPIES): thousands of waves ending together otherwise serialise on the same few words of
 // device-scope atomics (C2: 5,724 waves x up to 30 counters). The host reduces the copies.
 constexpr int CTR_COPIES = 64;
-constexpr int CTR_STRIDE = RAFT_CTR_COUNT + 2;   // 32 x u64 client-gap powers at the start of the block's LDS
+// one counter block: the RAFT_CTR_COUNT sums, then the first violation tick (MIN over waves) and
+// the largest append-entries payload (MAX over waves)
+constexpr int CTR_STRIDE = RAFT_CTR_COUNT + 2;
 
 struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
@@ -71,6 +73,7 @@ struct DevSim {
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
   uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
                             // delay: the LITE tick kernel applies
+  uint32_t* ovf;            // [NN][N-1][8] LDS-queue overflow cells (lite, N <= 5; else null)
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
@@ -238,9 +241,7 @@ __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
 }
 
 __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
-#ifndef RS_COST_NOCTR   // cost-attribution builds only (scripts/cost_probe.sh): results wrong
   if (v) atomicAdd(&lctr[i], v);
-#endif
 }
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own

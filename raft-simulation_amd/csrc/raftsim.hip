@@ -197,6 +197,11 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     return rc;
   }
   d.client_pw = s->client_pw;
+  d.ovf = nullptr;      // LDS-queue overflow cells: only the LITE kernel at N <= 5 uses them
+  if (s->N <= 5 && d.lite && (rc = dalloc(s, &d.ovf, NN * (s->N - 1) * 8))) {
+    sh_destroy(s);
+    return rc;
+  }
   d.wavelog = nullptr;
 #if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
   if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {
@@ -780,7 +785,13 @@ int raft_sim_set_tick(raft_sim_t* r, uint64_t tick) {
     const int rc = sh_sync(s);
     if (rc) return rc;
     s->tick = tick;
-    s->keys_fresh = false;      // the packing keys are relative to the next launch's first tick
+    // the packing keys are relative to the next launch's first tick: recompute them, and drop
+    // the histogram the last tick launch filled (sched_key_kernel only adds to it)
+    if (s->keys_fresh && s->d.shist) {
+      HIP_OK(hipSetDevice(s->cfg.device));
+      HIP_OK(hipMemsetAsync(s->d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream));
+    }
+    s->keys_fresh = false;
   }
   r->tick = tick;
   return 0;

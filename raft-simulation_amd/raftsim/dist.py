@@ -48,3 +48,12 @@ def reduce_max(x: float, device=None) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def reduce_sum(x: float, device=None) -> float:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

@@ -1,0 +1,9 @@
+# Targeted parity tests (pytest -k EXPR), then A/B of named builds (scripts/ab_probe.py).
+# Usage: bash scripts/gpu_ab_quick.sh "pytest -k expr" "libA libB ..." "--c2 ..."
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+B=raft-simulation_amd/build
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "$1" --timeout 300 --timeout-method thread > gpurun_out/quick_tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -30 gpurun_out/quick_tests.log
+[ $rc -eq 0 ] || exit 1
+L=""; for x in $2; do L="$L $B/$x.so"; done
+timeout -k 10 500 python -u scripts/ab_probe.py $L $3 > gpurun_out/ab.log 2>&1; rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab.log

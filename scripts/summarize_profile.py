@@ -32,9 +32,12 @@ KERNEL = "tick_kernel"
 def counters_by_kernel(path):
     """{kernel substring match -> {counter: [values per dispatch]}} from a counter_collection csv."""
     out = collections.defaultdict(lambda: collections.defaultdict(list))
+    rows = []
     for f in sorted(path.glob("**/*counter_collection.csv")):
-        for r in csv.DictReader(open(f)):
-            out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        rows.extend(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id") or 0))     # values in dispatch order
+    for r in rows:
+        out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return out
 
 
@@ -56,6 +59,15 @@ def calibration(src):
     return table
 
 
+def vgpr_compiler(tag, n):
+    """VGPRs of the tick-kernel instantiations at N = n from profiles/TAG_kernel_resources.txt."""
+    f = ROOT / "profiles" / f"{tag}_kernel_resources.txt"
+    if not f.exists():
+        return None
+    return {l[:48].strip(): int(l.split()[-4]) for l in f.read_text().splitlines()
+            if l.startswith(f"tick_kernel<N={n},")}
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r09"
     wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
@@ -75,7 +87,10 @@ def main():
             if KERNEL in kname:
                 for c, v in vals.items():
                     pmc[c].extend(v)
-    avg = {k: sum(v) / len(v) for k, v in pmc.items()}
+    # the timed launches only: the last `launches` dispatches of the tick kernel (warm-up
+    # launches, on the same or a throwaway handle, come first)
+    nl = max(1, bench["roofline"]["launches"])
+    avg = {k: sum(v[-nl:]) / len(v[-nl:]) for k, v in pmc.items()}
     trace = list(csv.DictReader(open(src / "kt" / "run_kernel_trace.csv")))
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
             if KERNEL in r["Kernel_Name"]]
@@ -84,6 +99,8 @@ def main():
     durs = durs[-max(1, bench["roofline"]["launches"]):]   # the timed launches, not the warm-up
     avg_ns = sum(durs) / max(1, len(durs))
 
+    n = bench["config"]["nodes"]
+    waves_ran = -(-bench["config"]["clusters_per_gpu"] // (64 // n))
     cal = calibration(src)
     (dst / f"{tag}_fetch_calibration.json").write_text(json.dumps(cal, indent=1) + "\n")
     roof = bench["roofline"]
@@ -106,7 +123,11 @@ def main():
         "launches_traced": len(durs), "avg_duration_ns_trace": avg_ns,
         "avg_duration_ns_stats": float(stats[0]["AverageNs"]) if stats else None,
         "bench_avg_launch_ms_hip_events": roof["avg_launch_ms"],
-        "vgpr": next((r.get("VGPR_Count") for r in trace if KERNEL in r["Kernel_Name"]), None),
+        # rocprofv3's VGPR_Count field is the allocation granule count of another encoding; the
+        # compiler's own register count is in profiles/TAG_kernel_resources.txt
+        "vgpr_rocprof_field": next((r.get("VGPR_Count") for r in trace
+                                    if KERNEL in r["Kernel_Name"]), None),
+        "vgpr_compiler": vgpr_compiler(tag, n),
         "pmc_per_launch": avg,
         # occupancy (MI355X_MICROARCH.md: SQ_WAVE_CYCLES in quad-cycles summed over waves;
         # GRBM_GUI_ACTIVE summed over the 8 XCDs): mean resident waves per CU over the
@@ -114,8 +135,15 @@ def main():
         "derived": {
             "mean_waves_per_cu": 4 * avg["SQ_WAVE_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 256)
             if avg.get("GRBM_GUI_ACTIVE") and "SQ_WAVE_CYCLES" in avg else None,
-            "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
-            if avg.get("SQ_WAVES") and "SQ_INSTS_VALU" in avg else None},
+            # SQ_WAVES counts every launched wave, including the waves past the packing's slots
+            # in use, which exit at once (the grid covers the padded packing's bound); per-wave
+            # figures divide by the waves that simulate clusters, ceil(clusters / (64 // N))
+            "waves_launched": avg.get("SQ_WAVES"),
+            "waves_with_clusters": waves_ran,
+            "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / waves_ran
+            if "SQ_INSTS_VALU" in avg else None,
+            "salu_insts_per_wave": avg["SQ_INSTS_SALU"] / waves_ran
+            if "SQ_INSTS_SALU" in avg else None},
         "calibration": {"k_read": k_rd, "k_write": k_wr, "state_read_weight": w_state,
                         "source": f"profiles/{tag}_fetch_calibration.json"},
         "hbm_fetch_bytes_raw": fetch_raw, "hbm_write_bytes_raw": write_raw,
@@ -137,7 +165,11 @@ def main():
         traffic = json.loads(tf.read_text())
     except (OSError, ValueError):
         traffic = {}
+    # the window the profiled bench run timed: bench.py attaches this traffic only to a line of the
+    # same window (a C3 window from init-node changes cost per launch as nodes halt)
     traffic[wl] = {"hbm_bytes_per_launch": hbm, "kernel_src_sha": roof["kernel_src_sha"],
+                   "window": bench.get("window"), "event_bytes_per_launch": event_bytes,
+                   "traffic_over_event_bytes": hbm / event_bytes if event_bytes else None,
                    "source": f"profiles/{tag}_{wl}_pmc.json"}
     tf.write_text(json.dumps(traffic, indent=1, sort_keys=True) + "\n")
     print(json.dumps({k: out[k] for k in ("workload", "avg_duration_ns_trace",

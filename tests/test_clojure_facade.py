@@ -44,3 +44,30 @@ def test_symbols_exist_in_header():
     declared = set(re.findall(r"\b(raft_sim_\w+)\s*\(", HEADER))
     assert used and used <= declared, used - declared
     assert "(def abi-version 2)" in CLJ and "#define RAFT_SIM_ABI_VERSION 2" in HEADER
+
+
+HARNESS = (ROOT / "clojure" / "src" / "raft" / "sim" / "harness.clj").read_text()
+
+
+def test_harness_word_arithmetic_is_unchecked():
+    """Clojure's checked long * and + throw on Philox-sized products and bit-shift-right is
+    arithmetic: the harness's 32-bit word arithmetic must use unchecked-multiply, unchecked-add and
+    unsigned-bit-shift-right ((* 0xD2511F53 c0) overflowed from round 2 on)."""
+    code = "\n".join(l.split(";")[0] for l in HARNESS.splitlines())   # strip comments
+    for op in ("(* ", "(+ ", "(bit-shift-right "):
+        assert op not in code, op
+    assert "(unchecked-multiply 0xD2511F53 c0)" in code
+    assert "(unsigned-bit-shift-right p1 32)" in code
+
+
+def test_harness_drives_every_phase():
+    """The per-tick cluster driver covers P0 (client injection), the D3 choice and one wait per
+    node (P1) with D8 halts, D4 re-arm, P2 delivery with the fault draws, and the D15 redirects."""
+    for name in ("defn- p0", "defn- p1", "defn- p2", "defn step-tick", "defn run-cluster",
+                 "defn canonical-nodes", "defn compare-golden", "halt-code", "timeout-deadline",
+                 "client-gap", ":client-abandoned", ":redirects", "P-NET", "P-PART"):
+        assert name in HARNESS, name
+    # the hooks SURVEY §8(b) names
+    for hook in ("server/incoming-rpc", "client/response-rpc", "core/generate-timeout",
+                 "client/rpc", "clojure.core/rand-nth", ":resp-chan"):
+        assert hook in HARNESS, hook

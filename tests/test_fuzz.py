@@ -86,3 +86,28 @@ def test_fuzz_gpu_drain(seed):
                trace_cap=0, trace_entry_cap=0)
     scns = [fuzz.random_scenario(rng, cfg) for _ in range(200)]
     _gpu_vs_oracle_multi_tick(cfg, scns, [8, 8, 64, 200])
+
+
+def _no_client_sets(scn):
+    """Drop queued client-sets: a host-written client-set turns the LITE kernel off."""
+    scn.queues = {q: [m for m in ms if m["type"] != "client-set"] for q, ms in scn.queues.items()}
+    scn.queues = {q: ms for q, ms in scn.queues.items() if ms}
+    return scn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_gpu_lite_queues(seed):
+    """LITE configurations (no client traffic, no faults, a fixed delay, N <= 5), where the tick
+    kernel keeps each launch's messages in LDS-resident queues: random states whose queued
+    messages start the launch in HBM mode, short timers and fixed delays up to 6 ticks (a sender
+    then finds its previous message still held: overflow cell + spill), tiny inboxes (LDS-mode
+    overflow drops), halted receivers; single-tick and long launches against the oracle."""
+    rng = random.Random(11000 + seed)
+    cfg = fuzz.random_config(rng)
+    d = rng.choice([1, 1, 2, 3, 6])
+    cfg.update(nodes=rng.randint(2, 5), client_ppm=0, drop_ppm=0, dup_ppm=0, part_ppm=0,
+               dmin=d, dmax=d, trace_cap=0, trace_entry_cap=0,
+               inbox_cap=rng.choice([1, 2, 3, 16]), variant_flags=rng.choice([0, 0, 1]))
+    scns = [_no_client_sets(fuzz.random_scenario(rng, cfg)) for _ in range(200)]
+    _gpu_vs_oracle_multi_tick(cfg, scns, [1, 3, 8, 64, 200, 2000])
