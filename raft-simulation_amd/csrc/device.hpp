@@ -73,7 +73,6 @@ struct DevSim {
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
   uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
                             // delay: the LITE tick kernel applies
-  uint32_t* ovf;            // [NN][N-1][8] LDS-queue overflow cells (lite, N <= 5; else null)
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
@@ -179,7 +178,6 @@ __device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const unsign
   const uint64_t j = P ? (uint64_t)(t / P) * B + t % P : t;
   return on_tick(j + 1 + client_gap(w, pw, top), P, B);
 }
-
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;
 }

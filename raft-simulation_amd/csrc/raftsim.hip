@@ -197,11 +197,6 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     return rc;
   }
   d.client_pw = s->client_pw;
-  d.ovf = nullptr;      // LDS-queue overflow cells: only the LITE kernel at N <= 5 uses them
-  if (s->N <= 5 && d.lite && (rc = dalloc(s, &d.ovf, NN * (s->N - 1) * 8))) {
-    sh_destroy(s);
-    return rc;
-  }
   d.wavelog = nullptr;
 #if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
   if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {

@@ -358,36 +358,13 @@ __device__ __forceinline__ void spec_handle(
   }
 }
 
-// LDS-resident queues (LQ; the LITE kernel at N <= 5, i.e. config 2). Messages between the nodes of
-// a cluster never leave the wave, so during a launch they stay in LDS instead of going through the
-// HBM rings: every (sender, receiver) pair owns one persistent 8-word cell holding a whole ring
-// message (arrival, hdr, term, a, b, eterm, eval, poff), and each queue of a node is the ordered
-// list of the senders whose cells it holds (3 bits per entry in one VGPR for both queues). A cell is
-// free while its hdr word is 0 (real headers are never 0). A pop reads the cell and frees it; P2
-// appends the senders of this tick's messages to the receiving list without touching memory.
-// Exactness: a sender holds at most one message per receiver in LDS, so a list never exceeds N - 1
-// entries. When a sender must emit to a receiver that still holds its previous message (a queue
-// backlog, or delay > hb), the new message goes to the pair's HBM overflow cell instead and the
-// receiver, in P2, spills both of its LDS lists to its HBM rings in order and then inserts the new
-// message there: the queue is in HBM mode (the general path) until it drains, when it returns to LDS
-// mode (ring head 0). Queues holding messages at launch start begin in HBM mode; LDS-mode queues
-// that still hold messages at launch end are written back to their rings (head 0), so the state
-// between launches is the canonical one.
-#ifndef RS_LQ
-#define RS_LQ 1
-#endif
-template <int N, bool LITE>
-constexpr bool lq() { return RS_LQ && LITE && N <= 5; }
-constexpr int LQW = 8;                                   // words per LQ cell
-constexpr uint32_t QL_HBM_REQ = 1u << 24, QL_HBM_RES = 1u << 25;   // queue in HBM mode
-
 // LDS words per wave: pair cells [cluster][sender][receiver other than the sender] of CELLW
-// words, then sender records [cluster][sender] of SRECW words (LQ: 8-word cells, no records),
-// counters, and (Spec-Raft) the wave's pre-tick arena frontiers.
-template <int N, bool LQ = false>
-constexpr int pair_words() { return (64 / N) * N * (N - 1) * (LQ ? LQW : CELLW); }
-template <int N, bool LQ = false>
-constexpr int cell_words() { return pair_words<N, LQ>() + (LQ ? 0 : (64 / N) * N * SRECW); }
+// words, then sender records [cluster][sender] of SRECW words, counters, and (Spec-Raft) the
+// wave's pre-tick arena frontiers.
+template <int N>
+constexpr int pair_words() { return (64 / N) * N * (N - 1) * CELLW; }
+template <int N>
+constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 // NM_LDS: the wave's next_index / match_index rows live in LDS during a launch ([2][N][64]
 // words), for the N whose block then still fits four per CU.
 #ifndef RS_NM_LDS
@@ -402,14 +379,14 @@ constexpr int RC_WORDS = 0;
 #endif
 // TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key)
 constexpr int TRIP_WORDS = 64;
-template <int N, bool SPEC, bool LQ = false>
+template <int N, bool SPEC>
 constexpr int wave_lds_words() {
-  return cell_words<N, LQ>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
+  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
          TRIP_WORDS + RC_WORDS;
 }
-template <int N, bool SPEC, bool LQ = false>
+template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + wave_lds_words<N, SPEC, LQ>()) * sizeof(uint32_t);
+  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
 }
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
@@ -454,17 +431,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
-  constexpr bool LQ = lq<N, LITE>();
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x;
   // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters and leader rows
   unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
   if (lane < 32) pw[lane] = S.client_pw[lane];
   uint32_t* cells = smem + PW_WORDS;
-  uint32_t* lctr = cells + cell_words<N, LQ>();
-  if constexpr (LQ) {                         // every LQ cell starts free (hdr word 0)
-    for (int i = lane; i < (64 / N) * N * (N - 1); i += 64) cells[i * LQW + 1] = 0;
-  }
+  uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
@@ -526,77 +499,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     }
   }
 
-  // LQ queue lists: REQ senders in bits 0-11, RES senders in bits 12-23 (3 bits per entry, head
-  // first, sender id 1..N), QL_HBM_* = the queue is in HBM mode. A queue holding messages at launch
-  // start is in HBM mode; an LDS-mode queue always has ring head 0.
-  uint32_t ql = 0;
-  if constexpr (LQ) {
-    ql = (n.rq.c ? QL_HBM_REQ : 0u) | (n.rs.c ? QL_HBM_RES : 0u);
-    if (!n.rq.c) n.rq.h = 0;                  // an empty ring's head is not state
-    if (!n.rs.c) n.rs.h = 0;
-  }
-  // LQ cell of the message from sender index s to receiver index r of the cluster at lanes b..
-  auto qcell = [&](int b, int s, int r) {
-    return cells + ((b + s) * (N - 1) + (r < s ? r : r - 1)) * LQW;
-  };
-  // Write the LDS list of queue `which` out to the node's HBM ring (slots 0..c-1, the LDS-mode
-  // head being 0), freeing its cells. The caller sets the HBM-mode bit or ends the launch.
-  auto lq_write_out = [&](int which, uint32_t xgi, int xk, int xbl) {
-    const QueueR q = which ? n.rs : n.rq;
-    uint32_t lst = (ql >> (which ? 12 : 0)) & 0xFFFu;
-    uint32_t* qb = qslots(S, xgi, which);
-    const size_t qs = qstride(S, which);
-    for (uint32_t i = 0; i < q.c; ++i, lst >>= 3) {
-      uint32_t* cl = qcell(xbl, (int)(lst & 7) - 1, xk);
-      const uint4 a = reinterpret_cast<const uint4*>(cl)[0], b = reinterpret_cast<const uint4*>(cl)[1];
-      cl[1] = 0;
-      uint4* dp = reinterpret_cast<uint4*>(qb + i * qs);
-      dp[0] = a;
-      dp[1] = b;
-    }
-    ql &= ~(0xFFFu << (which ? 12 : 0));
-  };
-  // The RES head (peek, either mode) and the next head's arrival; then the pop that commits it.
-  auto res_peek = [&](uint32_t xgi, int xk, int xbl, uint4& m0, uint4& m1) {
-    uint32_t narr = INF;
-    if (LQ && !(ql & QL_HBM_RES)) {
-      const uint32_t lst = (ql >> 12) & 0xFFFu;
-      const uint4* cl = reinterpret_cast<const uint4*>(qcell(xbl, (int)(lst & 7) - 1, xk));
-      m0 = cl[0];
-      m1 = cl[1];
-      if (n.rs.c > 1)
-        narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail
-                                                      : qcell(xbl, (int)((lst >> 3) & 7) - 1, xk)[0];
-    } else {
-      const uint32_t* qb = qslots(S, xgi, 1);
-      const size_t qs = qstride(S, 1);
-      const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
-      m0 = sp[0];
-      m1 = sp[1];
-      if (n.rs.c > 1)
-        narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail
-                                                      : qb[wrapq(n.rs.h + 1, S.Q) * qs];
-    }
-    return narr;
-  };
-  auto res_pop = [&](uint32_t narr, int xk, int xbl) {
-    QueueR r = n.rs;
-    if (LQ && !(ql & QL_HBM_RES)) {
-      const uint32_t lst = (ql >> 12) & 0xFFFu;
-      qcell(xbl, (int)(lst & 7) - 1, xk)[1] = 0;
-      ql = (ql & ~(0xFFFu << 12)) | (lst >> 3) << 12;
-      r.h = 0;
-    } else {
-      r.h = wrapq(r.h + 1, S.Q);
-      if (LQ && r.c == 1) ql &= ~QL_HBM_RES;
-    }
-    r.c -= 1;
-    r.arr = r.c ? narr : INF;
-    r.tail = r.c ? r.tail : 0u;
-    if (!r.c) r.h = 0;
-    n.rs = r;
-  };
-
   // Per-cluster reductions over the cluster's N lanes (every lane of the wave must be active).
   const uint32_t cmask = (1u << N) - 1;
   auto cluster_min = [&](uint32_t x) {
@@ -606,6 +508,31 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     return m;
   };
   auto cluster_any = [&](bool x) { return ((uint32_t)(__ballot(x) >> bl0) & cmask) != 0; };
+  const uint32_t tend = t0 + nt;
+  // Dead waves. A cluster whose every node is halted changes nothing but its client cursor and
+  // two counters from here on: a halt is permanent (D8) and a halted node drops what reaches it
+  // (core.clj:202-203), so its only events are client-sets into halted nodes (SIM_SPEC P0 + P2,
+  // to_halted). A wave holding only such clusters (the activity packing gives them waves of their
+  // own) runs their injections up to the launch's end here, one Philox draw each, with no trip;
+  // its trip loop then finds no event before tend. A wave that mixes live clusters in takes the
+  // trips (draining a dead cluster's injections there would stall its live wave mates).
+  if constexpr (!LITE && !SPEC) {
+    const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
+    if (S.client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
+      uint32_t cnt = 0;
+      while (active && cnext < tend) {
+        const uint4 d = philox(g, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
+        ++cnt;
+        ++ccount;
+        cnext = client_next_tick(cnext, d.w, pw, S.client_top, S.client_period, S.client_burst);
+      }
+      if (active && k0 == 0) {
+        lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
+        lctr_add(lctr, RAFT_CTR_TO_HALTED, cnt);
+      }
+    }
+  }
+
   // Earliest tick at which any node of the lane's cluster can have an event (deadline, queue head
   // or the next client-set), the same for all the cluster's lanes.
   auto next_event = [&]() {
@@ -626,11 +553,12 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     wl_kmin = wave_min(key);
     wl_kmax = ~wave_min(key == INF ? ~0u : ~key);
   }
-  // per-phase shader cycles summed over the wave's active ticks: loop top + P0, P1 up to the
-  // popped message's first use, P1 handler, P1 timer/trace/counters, redirect, emission, P2, P3,
-  // P4
+  // per-phase shader cycles summed over the wave's trips, stamped at wave-uniform points only:
+  // 0 P0, 3 P1, 4 P2, 5 P3, 6 P4, 7 the append-response drain, 8 the trip's loop head (next
+  // event, exit ballot); 9 the launch-start state load
   uint32_t wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t wl_ts = 0;
+  const uint64_t wl_mt0 = __builtin_amdgcn_s_memtime();
 #define RS_PHASE(i)                                          \
   do {                                                       \
     const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
@@ -641,7 +569,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #define RS_PHASE(i) do {} while (0)
 #endif
 
-  const uint32_t tend = t0 + nt;
+
   // Every cluster keeps its own clock. Ticks before a cluster's next event change nothing for it
   // (every handler, injection and delivery is keyed to a deadline, a queue head or the injection
   // cursor), and clusters never interact, so each trip of the loop runs every cluster's next
@@ -649,6 +577,10 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   // ticks, instead of the union of its clusters' event ticks (discrete-event skipping per
   // cluster, tick-exact; Philox draws are keyed by the cluster's own tick).
   uint32_t tnext = t0;                      // the cluster's first tick not yet simulated
+#ifdef RS_WAVELOG
+  wl_ts = __builtin_amdgcn_s_memtime();
+  wl_ph[9] = (uint32_t)(wl_ts - wl_mt0);
+#endif
   for (;;) {
     uint32_t t = max(tnext, next_event());
     t = t < tend ? t : tend;
@@ -657,7 +589,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     if (!LITE && S.client_ppm) tripsL[lane] += on;
     RS_RC(0);
 #ifdef RS_WAVELOG
-    wl_ts = __builtin_amdgcn_s_memtime();
+    RS_PHASE(8);
 #endif
     const bool live = on && !n.fault;
     // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
@@ -760,34 +692,17 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         // the ring is always in bounds) and used only when the queue stays non-empty.
         RS_RC(3);
         const QueueR q = which ? n.rs : n.rq;
-        const uint32_t hbit = which ? QL_HBM_RES : QL_HBM_REQ;
-        uint32_t nh, narr = INF;
-        if (LQ && !(ql & hbit)) {
-          // LQ pop: the head sender's cell (and the next head's arrival from the next cell)
-          const int sh = which ? 12 : 0;
-          const uint32_t lst = (ql >> sh) & 0xFFFu;
-          uint32_t* cl = qcell(bl, (int)(lst & 7) - 1, k);
-          m0 = reinterpret_cast<const uint4*>(cl)[0];
-          m1 = reinterpret_cast<const uint4*>(cl)[1];
-          if (q.c > 1)
-            narr = (q.c == 2 || q.arr == q.tail) ? q.tail
-                                                 : qcell(bl, (int)((lst >> 3) & 7) - 1, k)[0];
-          cl[1] = 0;
-          ql = (ql & ~(0xFFFu << sh)) | (lst >> 3) << sh;
-          nh = 0;
-        } else {
-          const uint32_t* qb = qslots(S, sgi, which);
-          const size_t qs = qstride(S, which);
-          const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
-          m0 = sp[0];
-          m1 = sp[1];
-          nh = wrapq(q.h + 1, S.Q);
-          // Only a queue that stays non-empty has a next head. Its arrival is known without a
-          // load when one message remains or all queued ones share the head's arrival (the queue
-          // is sorted, so head == tail means all equal): then nothing this tick waits on memory.
-          if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
-          if (LQ && q.c == 1) ql &= ~hbit;          // drained: back to LDS mode (head 0)
-        }
+        const uint32_t* qb = qslots(S, sgi, which);
+        const size_t qs = qstride(S, which);
+        const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
+        m0 = sp[0];
+        m1 = sp[1];
+        const uint32_t nh = wrapq(q.h + 1, S.Q);
+        // Only a queue that stays non-empty has a next head. Its arrival is known without a load
+        // when one message remains or all queued ones share the head's arrival (the queue is
+        // sorted, so head == tail means all equal): then nothing this tick waits on memory.
+        uint32_t narr = INF;
+        if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
         if (!have_w && n.role != RAFT_LEADER) {
           RS_RC(5);
           w = event_draw(sg, id, t, S);
@@ -810,7 +725,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 #ifdef RS_WAVELOG
       asm volatile("" ::"v"(hdr), "v"(mb));   // the pop's wait lands before the stamp
 #endif
-      RS_PHASE(1);
       const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
                      mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
       if constexpr (TRACE) {
@@ -1001,7 +915,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
       }
       const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
-      RS_PHASE(2);
       if (fault) {                                   // D8: halted with the pre-event state
         RS_RC(9);
         n.fault = fault;
@@ -1050,7 +963,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
           lctr_add(lctr, RAFT_CTR_LEADERS, 1);
           n.led = n.term;
         }
-        RS_PHASE(7);
         // ------------------------------------------------ redirect-client (server.clj:62-63)
         // to the :leader-id, else (rand-nth cluster) by w2 of the EVENT draw (core.clj:153-155);
         // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
@@ -1080,7 +992,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             sentmask |= 1u << dst;
           }
         }
-        RS_PHASE(8);
         // ------------------------------------------------ emission (rpc / respond)
         if (emit) {
           RS_RC(12);
@@ -1091,52 +1002,23 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             part = ppm(pw.x) < S.part_ppm;
             sides = pw.y;
           }
-          // LQ: the whole message (arrival after the fixed delay) into the pair's LDS cell, or
-          // into its HBM overflow cell when the receiver still holds this sender's previous
-          // message (bit 16 + receiver id: the receiver spills in P2); bit 31 = bound for RES.
-          auto lq_put = [&](int j, uint32_t p, bool busy) {
-            const uint4 a = make_uint4(t + S.dmin, ra.x, ra.y, ra.z),
-                        b = make_uint4(ra.w, rb.x, rb.y, rb.z);
-            uint4* dp = reinterpret_cast<uint4*>(
-                busy ? S.ovf + ((size_t)sgi * (N - 1) + j) * LQW
-                     : cells + ((bl + k) * (N - 1) + j) * LQW);
-            dp[0] = a;
-            dp[1] = b;
-            if (busy) sentmask |= 1u << (p + 16);
-          };
-          if constexpr (!LQ)
-            *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
-                emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
+          *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
+              emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
           if (emit == 3) {
             RS_RC(13);
-            const int j = src - 1 < (uint32_t)k ? (int)src - 1 : (int)src - 2;
-            RS_PHASE(9);
-            if constexpr (LQ) {
-              lq_put(j, src, cells[((bl + k) * (N - 1) + j) * LQW + 1] != 0);
-              sentmask |= 1u << src | 1u << 31;
-              lctr_add(lctr, RAFT_CTR_SENT, 1);
-            } else {
-              uint32_t* cl = mycells + (k * (N - 1) + j) * CELLW;
-              cell_put(cl, ra, rb);
-              lctr_add(lctr, RAFT_CTR_SENT, 1);
-              transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
-            }
-            RS_PHASE(10);
+            uint32_t* cl =
+                mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
+            cell_put(cl, ra, rb);
+            lctr_add(lctr, RAFT_CTR_SENT, 1);
+            transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
           } else {
             RS_RC(14);
-            RS_PHASE(9);
             // Message words first, for every peer at once: the next-index loads (and then the
             // prev-entry loads) of all peers are independent, so they overlap instead of paying
             // one memory round trip per peer; the fault draws follow in a compact loop.
             int32_t nxs[N];
 #pragma unroll
             for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? lsw.next(p) : 0;
-            uint32_t busy = 0;                // LQ: receivers still holding my previous message
-            if constexpr (LQ) {
-#pragma unroll
-              for (int j = 0; j < N - 1; ++j)
-                busy |= (cells[((bl + k) * (N - 1) + j) * LQW + 1] != 0 ? 1u : 0u) << j;
-            }
 #pragma unroll 1
             for (int p = 1; p <= N; ++p) {
               if (p == (int)id) continue;
@@ -1169,16 +1051,11 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                                 n.commit, (uint32_t)prev);
                 rb = make_uint4(et, evl, po, 0);
               }
-              const int j = p - 1 < k ? p - 1 : p - 2;
-              if constexpr (LQ) lq_put(j, (uint32_t)p, (busy >> j) & 1);
-              else cell_put(mycells + (k * (N - 1) + j) * CELLW, ra, rb);
+              cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
             }
-            RS_PHASE(11);
             if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
             lctr_add(lctr, RAFT_CTR_SENT, N - 1);
-            if constexpr (LQ) {
-              sentmask |= peers;
-            } else if constexpr (LITE) {   // every peer gets one copy after the fixed delay
+            if constexpr (LITE) {          // every peer gets one copy after the fixed delay
 #pragma unroll
               for (int j = 0; j < N - 1; ++j)
                 mycells[(k * (N - 1) + j) * CELLW + CELLW - 1] = S.dmin | 1u << 16;
@@ -1192,7 +1069,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
                             sentmask, lctr);
               }
             }
-            RS_PHASE(10);
           }
         }
       }
@@ -1200,68 +1076,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
 
     RS_PHASE(3);
     // ---------------------------------------------------------------- P2 network delivery
-    if constexpr (LQ) {
-      if (__ballot(sentmask != 0)) {
-        RS_RC(16);
-        // senders that addressed this lane (bits 0-4), which of them spilled to HBM (bits 8-12)
-        // and which queue each targets (bits 16-20: RES), in one word
-        uint32_t inm = 0;
-#pragma unroll
-        for (int s = 0; s < N; ++s) {
-          const uint32_t sm = __shfl(sentmask, bl + s);
-          inm |= (((sm >> id) & 1u) | ((sm >> (id + 16)) & 1u) << 8 | (sm >> 31) << 16) << s;
-        }
-        if (!on) inm = 0;
-        while (inm & 0xFFu) {                 // in sender id order (D6)
-          RS_RC(17);
-          const int s = __builtin_ctz(inm & 0xFFu);
-          const uint32_t bits = inm >> s;
-          inm &= ~(1u << s);
-          const int which = (bits >> 16) & 1;
-          const uint32_t hbit = which ? QL_HBM_RES : QL_HBM_REQ;
-          uint32_t* cl = qcell(bl, s, k);
-          QueueR q = which ? n.rs : n.rq;
-          if (!((bits >> 8) & 1) && !(ql & hbit)) {
-            // LDS-mode receiver: append the sender to the list; no memory traffic
-            if (n.fault) {
-              lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
-              cl[1] = 0;
-            } else if (q.c >= S.Q) {
-              lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
-              cl[1] = 0;
-            } else {
-              const uint32_t arr = t + S.dmin;
-              ql |= (uint32_t)(s + 1) << ((which ? 12 : 0) + 3 * q.c);
-              if (!q.c) q.arr = arr;
-              q.tail = arr;
-              q.c += 1;
-              lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-            }
-          } else {
-            uint4 m0, m1;
-            if ((bits >> 8) & 1) {
-              // the sender found its cell still held here: both LDS lists go to the HBM rings
-              // (in order), freeing every cell, and the message comes from the overflow cell
-              if (!(ql & QL_HBM_REQ) && n.rq.c) { lq_write_out(0, sgi, k, bl); ql |= QL_HBM_REQ; }
-              if (!(ql & QL_HBM_RES) && n.rs.c) { lq_write_out(1, sgi, k, bl); ql |= QL_HBM_RES; }
-              const uint4* ov = reinterpret_cast<const uint4*>(
-                  S.ovf + ((size_t)(sgi - k + s) * (N - 1) + (k < s ? k : k - 1)) * LQW);
-              m0 = ov[0];
-              m1 = ov[1];
-              q = which ? n.rs : n.rq;
-            } else {                          // HBM-mode receiver: the cell's message goes in
-              m0 = reinterpret_cast<const uint4*>(cl)[0];
-              m1 = reinterpret_cast<const uint4*>(cl)[1];
-              cl[1] = 0;
-            }
-            qinsert(S, sgi, n.fault, which, q, m0, m1, lctr);
-            if (q.c) ql |= hbit;
-          }
-          if (which) n.rs = q;
-          else n.rq = q;
-        }
-      }
-    } else if (__ballot(sentmask != 0)) {
+    if (__ballot(sentmask != 0)) {
       RS_RC(16);
       // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
       // copy per loop trip in (sender id, copy) order: a single qinsert call site for the wave.
@@ -1468,6 +1283,8 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         bool dr = on && any_res && any_ready && E > t + 1;
         if (__ballot(dr)) {
           RS_RC(25);
+          const uint32_t* qb = qslots(S, sgi, 1);
+          const size_t qs = qstride(S, 1);
           // A cluster with one eligible leader (the usual case) drains in that lane alone: its
           // ticks are the leader's own, so the loop needs no cluster reductions per tick. The
           // stop rules are the cluster loop's below: tau reaches E, a heartbeat falls due, or the
@@ -1479,14 +1296,24 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
               for (;;) {
                 const uint32_t tau = max(min(n.rs.arr, n.deadline), t + 1);
                 if (tau >= E || n.rs.arr > tau) break;       // E, or the heartbeat's tick
-                uint4 m0, m1;
-                const uint32_t narr = res_peek(sgi, k, bl, m0, m1);
+                const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
+                const uint4 m0 = sp[0], m1 = sp[1];
+                const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
+                uint32_t narr = INF;
+                if (n.rs.c > 1)
+                  narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
                 const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15,
                                flag = (hdr >> 7) & 1;
                 if (!((hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
                       (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1))))
                   break;
-                res_pop(narr, k, bl);
+                QueueR r = n.rs;
+                r.h = nh;
+                r.c -= 1;
+                r.arr = r.c ? narr : INF;
+                r.tail = r.c ? r.tail : 0u;
+                if (!r.c) r.h = 0;
+                n.rs = r;
                 if (flag) {                                // append-response-handler 145-149
                   n.lsp = 1;
                   n.keys |= 1u << src;
@@ -1514,7 +1341,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             const bool hbeat = dr && elig && !ev && n.deadline <= tau;
             uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
             uint32_t narr = INF;
-            if (ev) narr = res_peek(sgi, k, bl, m0, m1);
+            const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
+            if (ev) {
+              const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
+              m0 = sp[0];
+              m1 = sp[1];
+              if (n.rs.c > 1)
+                narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
+            }
             const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
             const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
                                 (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
@@ -1523,8 +1357,14 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
             if (!__ballot(dr)) break;
             RS_RC(26);
             if (dr && ev) {
-              res_pop(narr, k, bl);
-              if (flag) {                                // append-response-handler 145-149
+              QueueR r = n.rs;
+              r.h = nh;
+              r.c -= 1;
+              r.arr = r.c ? narr : INF;
+              r.tail = r.c ? r.tail : 0u;
+              if (!r.c) r.h = 0;
+              n.rs = r;
+              if (flag) {                                  // append-response-handler 145-149
                 n.lsp = 1;
                 n.keys |= 1u << src;
                 lsw.next(src - 1) = (int32_t)m1.x;
@@ -1545,6 +1385,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
         }
       }
     }
+    RS_PHASE(7);
     tnext = t + 1;
   }
 #ifdef RS_REGIONCOUNT
@@ -1581,9 +1422,13 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     // long as its busiest cluster (per-cluster clocks): clusters are then packed by how many
     // event ticks they ran in this launch, busiest first (they start first and are done before
     // the tail), instead of by their next event.
+    // The last bucket is kept for dead clusters (every node halted), which the next launch then
+    // packs into waves of their own and runs without trips (below the state load).
+    const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
     const uint32_t key = !head ? INF
                          : RS_PACK_ACTIVITY && S.client_ppm
-                             ? SCHED_BUCKETS - 1 - min(tripsL[lane], SCHED_BUCKETS - 1)
+                             ? (dead ? SCHED_BUCKETS - 1
+                                     : SCHED_BUCKETS - 2 - min(tripsL[lane], SCHED_BUCKETS - 2))
                              : sched_bucket(cm, tend);
     if (head) S.skey[c] = key;
     // a packed wave's clusters usually share their next key: one histogram atomic for the wave
@@ -1594,10 +1439,6 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
     } else if (head) {
       atomicAdd(&S.shist[key], 1u);
     }
-  }
-  if constexpr (LQ) {      // LDS-mode queues still holding messages go to their rings (head 0)
-    if (active && !(ql & QL_HBM_REQ) && n.rq.c) lq_write_out(0, gi, k0, bl0);
-    if (active && !(ql & QL_HBM_RES) && n.rs.c) lq_write_out(1, gi, k0, bl0);
   }
   if (active) {
     hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
@@ -1930,8 +1771,8 @@ void launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, h
     hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC, false>), dim3(waves), dim3(64), lds, st, ev0,
                           ev1, 0, S, t0, nt);
   else if (!SPEC && S.lite)
-    hipExtLaunchKernelGGL((tick_kernel<N, false, false, true>), dim3(waves), dim3(64),
-                          block_lds_bytes<N, false, lq<N, true>()>(), st, ev0, ev1, 0, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, false, false, true>), dim3(waves), dim3(64), lds, st, ev0,
+                          ev1, 0, S, t0, nt);
   else
     hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false>), dim3(waves), dim3(64), lds, st,
                           ev0, ev1, 0, S, t0, nt);
@@ -1964,7 +1805,7 @@ template <int N, bool TRACE, bool SPEC, bool LITE = false>
 hipError_t configure_one() {
   return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC, LITE>),
                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)block_lds_bytes<N, SPEC, lq<N, LITE>()>());
+                             (int)block_lds_bytes<N, SPEC>());
 }
 
 template <int N>

@@ -67,11 +67,15 @@ b = np.array(list(busy.values()))
 print("per-SIMD summed wave-us p0/50/100:", b.min(), np.median(b), b.max())
 per_xcc = [np.median(life[xcc == x]) for x in range(8)]
 print("per-XCC median life:", " ".join(f"{v:.1f}" for v in per_xcc))
-ph = a[:, [8, 9, 10, 15, 16, 17, 19, 18, 11, 12, 13, 14]].astype(np.float64)
+# wave-uniform phase stamps (shader cycles per wave, summed over its trips): rec[2..4] = ph0..11
+ph = a[:, [8, 11, 12, 13, 14, 15, 16]].astype(np.float64)
+names = ("P0", "P1", "P2", "P3", "P4", "drain", "loop-head")
 tot = ph.sum(axis=1)
-print("phase cycles per active tick (mean over waves): " + "  ".join(
-    f"{nm} {v:7.0f}" for nm, v in zip(("top+P0", "P1pop", "P1hdl", "P1timer", "P1redir", "emit-pre", "bcast-cells", "cells-xmit", "emit-post", "P2", "P3", "P4+next"),
-                                      (ph / np.maximum(act, 1)[:, None]).mean(axis=0))))
+trips = np.maximum(act, 1)[:, None]
+print("phase cycles per trip (mean over waves): " + "  ".join(
+    f"{nm} {v:7.0f}" for nm, v in zip(names, (ph / trips).mean(axis=0))))
+print("phase cycles per wave (mean): " + "  ".join(
+    f"{nm} {v:8.0f}" for nm, v in zip(names, ph.mean(axis=0))) + f"  load {a[:, 17].mean():8.0f}")
 print("drained ticks per wave p0/10/50/90/99/100:", q(a[:, 20]))
 print("client-injection ticks per wave p0/10/50/90/99/100:", q(a[:, 21]))
 print("dead clusters per wave at launch start p0/10/50/90/99/100:", q(a[:, 22]))

@@ -97,7 +97,8 @@ def oracle_idle_skip(be, on=True):
 
 
 def cpu_threads():
-    return max(1, min(16, os.cpu_count() or 1))
+    """Every CPU this process may run on (its affinity mask)."""
+    return max(1, len(os.sched_getaffinity(0)))
 
 
 def describe_cluster_diff(a, b, cluster):
