@@ -62,10 +62,10 @@ WORKLOADS = {
                cpu=(65536, 40),
                desc="C2: 65,536 five-node clusters per GPU x 10,000 ticks per step, no faults, "
                     "no client"),
-    "c3": dict(cfg=C3_CFG, clusters=1 << 20, scaling="strong", window="init", cpu=1 << 20,
+    "c3": dict(cfg=C3_CFG, clusters=1 << 20, scaling="strong", window="init", cpu=1 << 19,
                desc="C3: " + C3_DESC),
     "c3_spec": dict(cfg=dict(C3_CFG, variant_flags=2, log_cap=1024), clusters=1 << 20,
-                    scaling="strong", window="init", cpu=1 << 20,
+                    scaling="strong", window="init", cpu=1 << 19,
                     desc="C3 under the Spec-Raft control (SIM_SPEC §8, 1024-entry logs): "
                          + C3_DESC),
     "c4_n7": dict(cfg=dict(nodes=7, seed=3, log_cap=4096, client_ppm=500000, client_period=8192,
@@ -145,7 +145,7 @@ def cpu_baseline(spec, args):
 
     cfg = spec["cfg"]
     hc = host_cpus()
-    threads = hc["affinity"]
+    threads = helpers.cpu_threads()     # the affinity mask capped by the cgroup CPU quota
     if spec["window"] == "init":
         steps = args.steps
         clusters = max(1024, min(spec["clusters"], spec["cpu"] // max(1, steps)))
@@ -171,8 +171,9 @@ def cpu_baseline(spec, args):
              if not warm else f"{steps} steps after a warm-up step")
     return {"value": v, "unit": "node-ticks/s", "cores": threads, "kind": "port",
             "sample": f"{clusters} clusters x {cfg['nodes']} nodes, {where}, oracle/raftref.c "
-                      f"with the same idle-tick skipping as the kernel, {threads} threads (every "
-                      f"CPU in this process's affinity mask), {dt:.2f} s",
+                      f"with the same idle-tick skipping as the kernel, {threads} threads (the host "
+                      f"CPUs this process may use: affinity mask capped by the cgroup quota), "
+                      f"{dt:.2f} s",
             "host_cpus": hc,
             "every_tick_value": v_every,
             "every_tick_sample": f"{max(1, clusters // 8)} clusters x 1 step visiting every tick, "

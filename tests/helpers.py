@@ -97,8 +97,16 @@ def oracle_idle_skip(be, on=True):
 
 
 def cpu_threads():
-    """Every CPU this process may run on (its affinity mask)."""
-    return max(1, len(os.sched_getaffinity(0)))
+    """The host CPUs this process may use: its affinity mask, capped by the cgroup CPU quota (the
+    GPU box's share: its affinity mask shows every CPU of the machine, the quota 16 of them)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def describe_cluster_diff(a, b, cluster):
