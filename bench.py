@@ -79,7 +79,8 @@ WORKLOADS = {
                   desc="C4: 16,384 nine-node clusters, 4096-entry logs, bursty client "
                        "(1000+-entry batches)"),
 }
-KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip", "raft-simulation_amd/csrc/device.hpp",
+KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip", "raft-simulation_amd/csrc/steady_kernel.hip",
+                  "raft-simulation_amd/csrc/device.hpp",
                   "raft-simulation_amd/csrc/raftsim.hip", "include/raftsim.h"]
 HALTS = ("halt_ioobe", "halt_npe", "halt_cce", "halt_overflow")
 LIMITER = {

@@ -73,6 +73,14 @@ struct DevSim {
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
   uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
                             // delay: the LITE tick kernel applies
+  // Steady kernel hand-off (steady_kernel.hip): clusters it stops ("bails") at a tick it does not
+  // model are listed here, and the catch-up launch of the general kernel (perm = bail_c, nslots =
+  // nbail, resume = bail_t) runs them from that tick to the launch's end.
+  uint32_t* bail_c;         // [C] bailed cluster ids
+  uint32_t* bail_t;         // [C] the tick each bailed cluster stopped before
+  uint32_t* nbail;          // device word: clusters bailed this launch
+  uint32_t* nbail_zero;     // the next steady launch's word (two alternate), zeroed by this one
+  const uint32_t* resume;   // general kernel: per wave slot, the tick its cluster resumes at
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
@@ -96,6 +104,18 @@ __device__ __forceinline__ uint32_t* hot_cl(const DevSim& S, uint32_t c) {
 
 constexpr uint32_t SCHED_BUCKETS = 16384;   // keys clamp to SCHED_BUCKETS - 1
 constexpr uint32_t SCHED_PAST = 16;         // bucket of "now": keys keep 16 ticks of past
+
+// The histogram bucket of a cluster whose next event is `ev`, for a launch starting at t0. Events
+// up to SCHED_PAST ticks in the past (messages that arrived but wait behind others, e.g. a
+// leader's remaining append-responses in mid round) keep their tick: they tell a cluster that is
+// 3 ticks into a heartbeat round from one that starts a round at t0, whose later rounds would
+// otherwise stay 3 ticks apart in the same wave.
+__device__ __forceinline__ uint32_t sched_bucket(uint32_t ev, uint32_t t0) {
+  const uint64_t k = (uint64_t)ev + SCHED_PAST;
+  if (k <= t0) return 0;
+  const uint64_t d = k - t0;
+  return d < SCHED_BUCKETS - 1 ? (uint32_t)d : SCHED_BUCKETS - 1;
+}
 
 // Slots the padded wave packing may use (RAFT_SCHED_ALIGNED): twice the clusters plus one partial
 // wave per plan chunk (SCHED_PLAN_CHUNKS), so the unpadded fallback always fits; the tick kernel's
@@ -180,6 +200,23 @@ __device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const unsign
 }
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;
+}
+
+__device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t ev, uint32_t src,
+                                                uint32_t mterm, uint32_t role, uint32_t term,
+                                                uint32_t fault) {
+  h = fnv(h, t);
+  h = fnv(h, ev);
+  h = fnv(h, src);
+  h = fnv(h, mterm);
+  h = fnv(h, role);
+  h = fnv(h, term);
+  return fnv(h, fault);
+}
+
+// The EVENT draw of node id at tick t (SIM_SPEC §3): alts!! bit, timeout, rand-nth peer.
+__device__ __forceinline__ uint4 event_draw(uint32_t g, uint32_t id, uint32_t t, const DevSim& S) {
+  return philox(g, id | P_EVENT << 8, t, 0, S.key0, S.key1);
 }
 
 // Flags word: role 0-1 | voted_for 2-5 | leader_id 6-9 | fault 10-12 | is_seq 13 | ls_present 14

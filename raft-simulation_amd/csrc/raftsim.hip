@@ -10,7 +10,7 @@
 
 namespace rs {
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
-                       hipEvent_t ev1);
+                       hipEvent_t ev1, bool steady);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
                              hipStream_t st);
@@ -60,7 +60,16 @@ struct Shard {
   uint32_t *soff, *sperm, *snslots;   // + the slot count of the packing
   bool keys_fresh;
   uint64_t resort_ctr = 0;             // tick launches since create (RS_RESORT_EVERY)
+  // steady kernel (steady_kernel.hip): LITE launches at N <= 5 without TRACE; the two bail
+  // counters alternate between launches (each steady launch zeroes the other)
+  bool steady_ok;
+  uint32_t* nbail2;
+  uint32_t steady_parity;
 };
+// 0: LITE launches always take the general kernel (A/B builds); results are the same either way
+#ifndef RS_STEADY
+#define RS_STEADY 1
+#endif
 // The wave packing is rebuilt every RS_RESORT_EVERY-th tick launch and reused in between: with
 // key-pure waves a steady-state cluster keeps its wave mates' phase, so a packing stays good for
 // more than one 10k-tick launch, and skipping the schedule kernel (C2: 14.6 us) every other
@@ -204,6 +213,12 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     return rc;
   }
 #endif
+  s->steady_ok = RS_STEADY && d.lite && s->N <= 5 && !d.TC && !(cfg->variant_flags & RAFT_VARIANT_SPEC);
+  if (s->steady_ok && ((rc = dalloc(s, &d.bail_c, s->C)) || (rc = dalloc(s, &d.bail_t, s->C)) ||
+                       (rc = dalloc(s, &s->nbail2, 2)))) {
+    sh_destroy(s);
+    return rc;
+  }
   if (cfg->schedule == RAFT_SCHED_ALIGNED) {
     if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
         (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) ||
@@ -227,6 +242,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
       (e = hipMemsetAsync(d.tent, 0, NN * std::max<uint32_t>(d.TE, 1) * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tecount, 0, NN * 4, s->stream)) != hipSuccess ||
       (d.shist && (e = hipMemsetAsync(d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream)) != hipSuccess) ||
+      (s->nbail2 && (e = hipMemsetAsync(s->nbail2, 0, 8, s->stream)) != hipSuccess) ||
       (e = init_counters(s)) != hipSuccess ||
       (e = hipMemcpyAsync(s->client_pw, pw, sizeof pw, hipMemcpyHostToDevice, s->stream)) !=
           hipSuccess ||
@@ -282,7 +298,14 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
                           (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
 #endif
-    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1]));
+    const bool steady = s->steady_ok && s->d.lite;   // host writes may have cleared lite
+    if (steady) {
+      s->d.nbail = s->nbail2 + s->steady_parity;
+      s->d.nbail_zero = s->nbail2 + (s->steady_parity ^ 1);
+      s->steady_parity ^= 1;
+    }
+    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1],
+                           steady));
     if (keep_hist) s->d.shist = keep_hist;
     done += nt;
     s->tick += nt;

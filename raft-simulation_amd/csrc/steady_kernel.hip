@@ -1,0 +1,368 @@
+// steady_kernel.hip — the steady-state tick kernel of LITE launches for gfx950 (MI355X).
+//
+// In a LITE launch (no client traffic, no faults, fixed delay: BASELINE config 2) a cluster that
+// has elected its leader repeats one heartbeat round forever: the leader's heartbeat broadcasts an
+// empty append-entries (heartbeat-handler, core.clj:162-164; append-entries-rpc 56-67), every
+// follower answers it (append-entries-handler 105-123) and the leader takes the answers, one per
+// tick (append-response-handler 141-149). This kernel runs exactly those events, bit for bit as
+// the general tick kernel does (SIM_SPEC.md §4), and nothing else: a cluster about to run any other
+// event (an election, a log entry, a halt, a message it cannot hold) is stopped ("bailed") before
+// that tick with its state written back, and the catch-up launch of the general kernel runs it from
+// that tick to the launch's end (DevSim::bail_c / bail_t / nbail). Results are therefore identical
+// to the general kernel's for any state; only the speed depends on how steady the clusters are.
+//
+// What the narrow event set buys: no log arena, no HBM queue traffic and a small register set.
+// * Queues live in LDS for the whole launch. Every ordered (sender, receiver) pair of a cluster
+//   owns one 4-word cell (arrival, term, a, b | hdr << 24); a node's REQ and RES queues are lists of
+//   sender ids (4 bits each) in one VGPR. A message whose pair cell is still occupied, or one the
+//   cell cannot express (entries, a payload reference, b >= 2^24), bails its cluster. The HBM rings
+//   are read at launch start and written at the end (heads at slot 0; ring positions are not state).
+// * The leader-state rows (next-index / match-index) of the cluster's one ls_present node live in
+//   LDS; the other nodes' rows are never touched (a second ls_present node bails the cluster).
+// * Log length, arena cursors, last-led term and commit counts cannot change here, so they are
+//   neither loaded nor stored.
+// Registers: ~60 VGPRs against the general kernel's 117, so a wave slot per SIMD more than the
+// whole config-2 grid needs: one generation of waves instead of two.
+#include <hip/hip_ext.h>
+
+#include "device.hpp"
+
+namespace rs {
+
+constexpr int SCW = 4;   // words per pair cell: arrival, term, a, b | hdr << 24 (free: word 3 == 0)
+
+template <int N>
+constexpr int steady_cells() { return (64 / N) * N * (N - 1); }
+template <int N>
+constexpr size_t steady_lds_bytes() {
+  return (size_t)(steady_cells<N>() * SCW + (64 / N) * 2 * N + LCTR_WORDS) * sizeof(uint32_t);
+}
+
+// fl bits kept beside the packed flags word (pack_flags) while the kernel runs
+constexpr uint32_t SF_ACKBAD = 1u << 15;   // log_len > checker hwm: a success response is a check
+
+template <int N>
+__global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+  static_assert(N >= 2 && N <= 5, "4-bit sender lists of at most four entries");
+  constexpr int CPW = 64 / N;
+  constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
+  constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* const cells = smem;                                   // [CPW*N][N-1][SCW]
+  int32_t* const rows = reinterpret_cast<int32_t*>(smem + steady_cells<N>() * SCW);  // [CPW][2N]
+  uint32_t* const lctr = smem + steady_cells<N>() * SCW + CPW * 2 * N;
+  const int lane = threadIdx.x;
+  if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+  if (blockIdx.x == 0 && lane == 0) *S.nbail_zero = 0;   // the bail counter of the next launch
+
+  const uint32_t wave = blockIdx.x;
+  const uint32_t nslots = S.perm ? *S.nslots : S.C;
+  if (wave * CPW >= nslots) return;
+  const int cs = lane / N, k = lane - cs * N;
+  const uint32_t slot = wave * CPW + cs;
+  const uint32_t c0 = lane < CPW * N && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
+  const bool active = c0 != INF;
+  const uint32_t c = active ? c0 : 0u;
+  const uint32_t g = S.goff + c, gi = c * N + k, id = k + 1;
+  const int bl = (cs < CPW ? cs : 0) * N;
+  const uint32_t peers = ALL & ~(1u << id);
+  const uint32_t cmask = (1u << N) - 1;
+  uint32_t* const hp = S.hot + (size_t)c * HB + k;
+  uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
+  int32_t* const myrows = rows + cs * 2 * N;                     // next[N], then match[N]
+  // this lane's pair cells: outgoing (to receiver index j) and incoming (from sender index s)
+  auto cell_out = [&](int j) { return cells + ((bl + k) * (N - 1) + (j < k ? j : j - 1)) * SCW; };
+  auto cell_in = [&](int s) { return cells + ((bl + s) * (N - 1) + (k < s ? k : k - 1)) * SCW; };
+  if (lane < CPW * N) {            // every pair cell starts free
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) cells[(lane * (N - 1) + j) * SCW + 3] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  auto cluster_any = [&](bool x) { return ((uint32_t)(__ballot(x) >> bl) & cmask) != 0; };
+  auto cluster_min = [&](uint32_t x) {
+    uint32_t m = x;
+#pragma unroll
+    for (int s = 0; s < N; ++s) m = min(m, (uint32_t)__shfl(x, bl + s));
+    return m;
+  };
+
+  // ------------------------------------------------------------------ state load (launch start)
+  uint32_t fl = 0, mk = 0, term = 0, commit = 0, len = 0, deadline = INF, rqa = INF, rsa = INF;
+  uint32_t lists = 0;             // REQ senders (id) in nibbles 0-3, RES senders in nibbles 4-7
+  uint64_t trace = 0;
+  bool bad = false;               // the cluster's start state is outside this kernel's model
+  if (active) {
+    fl = hp[HF_FLAGS * N]; mk = hp[HF_MASKS * N];
+    term = hp[HF_TERM * N]; commit = hp[HF_COMMIT * N]; len = hp[HF_LEN * N];
+    deadline = hp[HF_DEADLINE * N];
+    const uint32_t qm = hp[HF_QMETA * N];
+    rqa = hp[HF_REQ_ARR * N]; rsa = hp[HF_RES_ARR * N];
+    trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
+    if (len > hc[0]) fl |= SF_ACKBAD;
+    // queued messages into the pair cells, in ring order
+    const uint32_t rqh = qm & 15, rqc = (qm >> 4) & 31, rsh = (qm >> 9) & 15, rsc = (qm >> 13) & 31;
+    if (rqc + rsc > N - 1) bad = true;
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < rqc + rsc && !bad; ++i) {
+      const bool res = i >= rqc;
+      const uint32_t pos = wrapq((res ? rsh + i - rqc : rqh + i), S.Q);
+      const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, gi, res) + pos * qstride(S, res));
+      const uint4 m0 = mp[0], m1 = mp[1];
+      const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
+      if ((hdr >> 8) || m1.y || m1.z || m1.w || m1.x >= (1u << 24) || src < 1 || src > N ||
+          src == id || ((used >> src) & 1) || m0.x > t0 + S.dmin) {
+        bad = true;
+      } else {
+        used |= 1u << src;
+        *reinterpret_cast<uint4*>(cell_in(src - 1)) = make_uint4(m0.x, m0.z, m0.w, m1.x | hdr << 24);
+        const uint32_t n = res ? i - rqc : i;
+        lists |= src << (4 * n + (res ? 16 : 0));
+      }
+    }
+  }
+  // the leader-state rows of the cluster's ls_present node (at most one)
+  const bool lsp = active && ((fl >> 14) & 1);
+  const uint32_t lspm = (uint32_t)(__ballot(lsp) >> bl) & cmask;
+  bad = bad || __popc(lspm) > 1;
+  if (lsp) {
+#pragma unroll
+    for (int p = 0; p < 2 * N; ++p) myrows[p] = (int32_t)hp[(HF_NEXT + p) * N];
+  }
+  // a cluster outside the model from the start bails at t0 with its state untouched
+  const bool bad0 = cluster_any(bad);
+  if (active && bad0 && k == 0) {
+    const uint32_t i = atomicAdd(S.nbail, 1u);
+    S.bail_c[i] = c;
+    S.bail_t[i] = t0;
+  }
+  const bool wb = active && !bad0;          // state to write back at the end
+  bool run = wb;                            // the cluster still runs here (not bailed)
+  __builtin_amdgcn_wave_barrier();
+
+  const uint32_t tend = t0 + nt, d = S.dmin;
+  uint32_t tnext = t0;
+  for (;;) {
+    const bool liv0 = run && !((fl >> 10) & 7);
+    uint32_t t = max(tnext, cluster_min(liv0 ? min(deadline, min(rqa, rsa)) : INF));
+    t = t < tend ? t : tend;
+    const bool on = run && t < tend;
+    if (!__ballot(on)) break;
+    const bool live = on && !((fl >> 10) & 7);
+    const uint32_t role = fl & 3;
+    const bool rqok = live && rqa <= t, rsok = live && rsa <= t;
+    const bool ev = rqok || rsok || (live && t >= deadline);
+    // ------------------------------------------------ decide (no state changes yet)
+    // The EVENT draw: for the alts!! choice when both queues are ready, and for the next election
+    // timeout of a node that is not leader after the event (a follower's append-entries, a
+    // leader's append-entries of a newer term; core.clj:171-174).
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (ev && (rqok || role != RAFT_LEADER)) w = event_draw(g, id, t, S);
+    const int which = rqok && rsok ? (int)(w.x & 1) : rqok ? 0 : rsok ? 1 : -1;
+    const int s = which >= 0 ? (int)((lists >> (which ? 16 : 0)) & 15) - 1 : 0;
+    uint4 m = make_uint4(0, 0, 0, 0);
+    if (which >= 0) m = *reinterpret_cast<const uint4*>(cell_in(s));
+    const uint32_t mterm = m.y, ma = m.z, mb = m.w & 0xFFFFFFu, hdr = m.w >> 24;
+    const uint32_t type = hdr & 7, flag = (hdr >> 7) & 1, src = (uint32_t)s + 1;
+    const uint32_t keys = mk >> 16;
+    bool ok = true;
+    if (ev) {
+      if (which < 0) {
+        // heartbeat: leader with full leader-state, no LazySeq log, commit within the log (the
+        // IOOBE/NPE/CCE checks of append-entries-rpc pass), an empty broadcast (every peer's
+        // prev-index at or past the log's end) and every outgoing cell free
+        ok = role == RAFT_LEADER && ((fl >> 14) & 1) && (keys & peers) == peers &&
+             !((fl >> 13) & 1) && commit <= len;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          if (j == k) continue;
+          const int32_t nx = myrows[j];
+          const uint32_t prev = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
+          ok = ok && prev >= len && prev < (1u << 24) && cell_out(j)[3] == 0;
+        }
+      } else if (which == 0) {
+        // append-entries with prev-index 0 and no entries (consistent without a log read); a
+        // newer term sets commit = log_len, which applies nothing when commit >= log_len
+        ok = type == RAFT_MSG_APPEND_ENTRIES && mb == 0 && (mterm < term || len <= commit) &&
+             cell_out(s)[3] == 0;
+      } else {
+        // append-response of no newer term to the row owner; a success response is checker
+        // work once the log passes the hwm (P4)
+        ok = type == RAFT_MSG_APPEND_RESPONSE && ((fl >> 14) & 1) && mterm <= term &&
+             (flag ? !(fl & SF_ACKBAD) : ((keys >> src) & 1) != 0);
+      }
+    }
+    if (cluster_any(ev && !ok)) {           // bail before this tick: the general kernel runs it
+      if (on && k == 0) {
+        const uint32_t i = atomicAdd(S.nbail, 1u);
+        S.bail_c[i] = c;
+        S.bail_t[i] = t;
+      }
+      run = false;
+      continue;
+    }
+    // ------------------------------------------------ run the event
+    uint32_t sent = 0;             // receivers (bits 1..N); bit 31: replies (RES queues)
+    if (ev) {
+      uint32_t evc, tsrc = 0, tterm = 0;
+      if (which >= 0) {            // pop the head: free the cell, next head's arrival
+        cell_in(s)[3] = 0;
+        const int sh = which ? 16 : 0;
+        const uint32_t rest = ((lists >> sh) & 0xFFFFu) >> 4;
+        lists = (lists & ~(0xFFFFu << sh)) | rest << sh;
+        const uint32_t na = rest ? cell_in((int)(rest & 15) - 1)[0] : INF;
+        if (which) rsa = na;
+        else rqa = na;
+        tsrc = src;
+        tterm = mterm;
+      }
+      if (which < 0) {             // heartbeat-handler: append-entries to every peer
+        evc = 7;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          if (j == k) continue;
+          const int32_t nx = myrows[j];
+          const uint32_t prev = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
+          *reinterpret_cast<uint4*>(cell_out(j)) =
+              make_uint4(t + d, term, commit, prev | (RAFT_MSG_APPEND_ENTRIES | id << 3) << 24);
+        }
+        sent = peers;
+        lctr_add(lctr, RAFT_CTR_SENT, N - 1);
+      } else if (which == 0) {     // append-entries-handler
+        evc = RAFT_MSG_APPEND_ENTRIES;
+        uint32_t rh = RAFT_MSG_APPEND_RESPONSE | id << 3, ra = 0;
+        const uint32_t rterm = term;
+        if (mterm >= term) {
+          rh |= 1u << 7;
+          ra = ma;
+          commit = len;                                   // apply-entries! (nothing applied)
+          term = mterm;
+          // role :follwer, voted-for and votes cleared, leader-id = src, LazySeq flag cleared
+          fl = (fl & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER | src << 6;
+          mk &= 0xFFFF0000u;
+        }
+        *reinterpret_cast<uint4*>(cell_out(s)) = make_uint4(t + d, rterm, ra, rh << 24);
+        sent = 1u << src | 1u << 31;
+        lctr_add(lctr, RAFT_CTR_SENT, 1);
+      } else {                     // append-response-handler
+        evc = RAFT_MSG_APPEND_RESPONSE;
+        if (flag) {
+          mk |= 1u << (16 + src);
+          myrows[s] = (int32_t)mb;
+          myrows[N + s] = (int32_t)ma;
+        } else {
+          myrows[s] -= 1;
+        }
+      }
+      const uint32_t r2 = fl & 3;
+      deadline = r2 == RAFT_LEADER ? t + S.hb : t + S.el_base + __umulhi(w.y, S.el_span);
+      trace = trace_event(trace, t, evc, tsrc, tterm, r2, term, 0);
+      lctr_add(lctr, RAFT_CTR_EV_RV + evc - 1, 1);
+    }
+    // ------------------------------------------------ P2: deliveries, in sender id order
+    if (__ballot(sent != 0)) {
+      uint32_t inm = 0, rep = 0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const uint32_t sm = __shfl(sent, bl + j);
+        inm |= ((sm >> id) & 1u) << j;
+        rep |= (sm >> 31) << j;
+      }
+      if (!on) inm = 0;              // padding lanes alias cluster 0's lanes
+      while (inm) {
+        const int j = __builtin_ctz(inm);
+        inm &= inm - 1;
+        const int sh = ((rep >> j) & 1) ? 16 : 0;
+        const uint32_t q = (lists >> sh) & 0xFFFFu;
+        const uint32_t cnt = q ? (35u - __clz(q)) >> 2 : 0u;     // nibbles in use
+        if ((fl >> 10) & 7) {
+          lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
+          cell_in(j)[3] = 0;
+        } else if (cnt >= S.Q) {
+          lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
+          cell_in(j)[3] = 0;
+        } else {
+          lists |= (uint32_t)(j + 1) << (sh + 4 * cnt);
+          if (!cnt) {
+            if (sh) rsa = t + d;
+            else rqa = t + d;
+          }
+          lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+        }
+      }
+    }
+    tnext = t + 1;
+  }
+
+  // ------------------------------------------------------------------ write back
+  if (S.shist) {
+    // packing key for the next launch (as the general kernel's, keys of running clusters only:
+    // a bailed cluster's key comes from the catch-up launch)
+    const uint32_t me = wb && !((fl >> 10) & 7) ? min(deadline, min(rqa, rsa)) : INF;
+    const uint32_t cm = cluster_min(me);
+    const bool head = wb && run && k == 0;
+    const uint32_t key = head ? sched_bucket(cm, tend) : INF;
+    if (head) S.skey[c] = key;
+    const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
+    const uint32_t heads = (uint32_t)__popcll(__ballot(head));
+    if (kmin == kmax) {
+      if (lane == 0 && kmin != INF) atomicAdd(&S.shist[kmin], heads);
+    } else if (head) {
+      atomicAdd(&S.shist[key], 1u);
+    }
+  }
+  if (wb) {
+    hp[HF_FLAGS * N] = fl & ~SF_ACKBAD;
+    hp[HF_MASKS * N] = mk;
+    hp[HF_TERM * N] = term; hp[HF_COMMIT * N] = commit; hp[HF_DEADLINE * N] = deadline;
+    hp[HF_TRACE_LO * N] = (uint32_t)trace; hp[HF_TRACE_HI * N] = (uint32_t)(trace >> 32);
+    // queues back to the rings, heads at slot 0; tail = the last message's arrival (0 if empty)
+    uint32_t cnt[2] = {0, 0}, tail[2] = {0, 0};
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      uint32_t q = (lists >> (which ? 16 : 0)) & 0xFFFFu;
+      uint32_t* qb = qslots(S, gi, which);
+      const size_t qs = qstride(S, which);
+      for (uint32_t i = 0; q; ++i, q >>= 4) {
+        const uint32_t sj = (q & 15) - 1;
+        const uint4 x = *reinterpret_cast<const uint4*>(cell_in((int)sj));
+        uint4* dp = reinterpret_cast<uint4*>(qb + i * qs);
+        dp[0] = make_uint4(x.x, x.w >> 24, x.y, x.z);
+        dp[1] = make_uint4(x.w & 0xFFFFFFu, 0, 0, 0);
+        cnt[which] = i + 1;
+        tail[which] = x.x;
+      }
+    }
+    hp[HF_QMETA * N] = pack_qmeta(0, cnt[0], 0, cnt[1]);
+    hp[HF_REQ_ARR * N] = rqa; hp[HF_RES_ARR * N] = rsa;
+    hp[HF_REQ_TAIL * N] = tail[0]; hp[HF_RES_TAIL * N] = tail[1];
+    if (lsp) {
+#pragma unroll
+      for (int p = 0; p < 2 * N; ++p) hp[(HF_NEXT + p) * N] = (uint32_t)myrows[p];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  unsigned long long* const ctr = S.ctr + (size_t)(wave % CTR_COPIES) * CTR_STRIDE;
+  if (lane < RAFT_CTR_COUNT) {
+    const uint32_t v = lctr[lane];
+    if (v) atomicAdd(&ctr[lane], (unsigned long long)v);
+  }
+}
+
+// The steady kernel for N <= 5 (LITE launches; the caller checks). Grid: the packing's slots.
+hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, uint32_t waves, hipStream_t st,
+                         hipEvent_t ev0) {
+  switch (S.N) {
+#define RS_STEADY(NN)                                                                            \
+  case NN:                                                                                       \
+    hipExtLaunchKernelGGL((steady_kernel<NN>), dim3(waves), dim3(64), steady_lds_bytes<NN>(), st, \
+                          ev0, nullptr, 0, S, t0, nt);                                          \
+    break;
+    RS_STEADY(2) RS_STEADY(3) RS_STEADY(4) RS_STEADY(5)
+#undef RS_STEADY
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace rs
