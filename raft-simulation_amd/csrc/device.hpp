@@ -81,6 +81,8 @@ struct DevSim {
   uint32_t* nbail;          // device word: clusters bailed this launch
   uint32_t* nbail_zero;     // the next steady launch's word (two alternate), zeroed by this one
   const uint32_t* resume;   // general kernel: per wave slot, the tick its cluster resumes at
+  uint32_t* bail_report;    // host-mapped word: the catch-up launch stores its cluster count there
+                            // (the host picks the next launches' path from it; speed only)
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer

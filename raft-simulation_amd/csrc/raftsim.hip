@@ -1,5 +1,6 @@
 // raftsim.hip — C ABI of libraftsim.so (include/raftsim.h) over the gfx950 tick kernel.
 #include <errno.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -63,9 +64,19 @@ struct Shard {
   // steady kernel (steady_kernel.hip): LITE launches at N <= 5 without TRACE; the two bail
   // counters alternate between launches (each steady launch zeroes the other)
   bool steady_ok;
+  bool last_steady;                    // the last tick launch took the steady path
   uint32_t* nbail2;
   uint32_t steady_parity;
+  // Path choice per launch (speed only: both paths give the same state). RAFTSIM_STEADY=auto
+  // (default): the steady kernel unless the last catch-up launch the host has seen (bail_host,
+  // written by the GPU; a few launches stale at most) took more than 1/16 of the clusters, then
+  // the general kernel for the next STEADY_COOLDOWN launches; the first launch of a handle
+  // (init-node: every cluster still has to elect) is general. "always" / "never" force a path.
+  int steady_mode;                     // 0 auto, 1 always, 2 never
+  uint32_t* bail_host;                 // host-mapped word (hipHostMalloc)
+  uint32_t steady_cooldown;
 };
+constexpr uint32_t STEADY_COOLDOWN = 2;
 // 0: LITE launches always take the general kernel (A/B builds); results are the same either way
 #ifndef RS_STEADY
 #define RS_STEADY 1
@@ -77,6 +88,12 @@ struct Shard {
 // further gain). Results never depend on the packing.
 #ifndef RS_RESORT_EVERY
 #define RS_RESORT_EVERY 2
+#endif
+// LITE launches: a steady-state packing is a rotation of itself one launch later (every cluster's
+// next event moves by the same launch length), so after the first 8 launches (elections) it is
+// rebuilt less often
+#ifndef RS_RESORT_EVERY_LITE
+#define RS_RESORT_EVERY_LITE 8
 #endif
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
@@ -145,6 +162,7 @@ static void sh_destroy(Shard* s) {
   (void)hipSetDevice(s->cfg.device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : s->allocs) (void)hipFree(p);
+  if (s->bail_host) (void)hipHostFree(s->bail_host);
   if (s->ev_start) (void)hipEventDestroy(s->ev_start);
   if (s->ev_stop) (void)hipEventDestroy(s->ev_stop);
   for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);
@@ -219,6 +237,20 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     sh_destroy(s);
     return rc;
   }
+  if (s->steady_ok) {
+    const char* m = getenv("RAFTSIM_STEADY");
+    s->steady_mode = m && !strcmp(m, "always") ? 1 : m && !strcmp(m, "never") ? 2 : 0;
+    s->steady_cooldown = 1;
+    void* hp = nullptr;
+    if (hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d.bail_report), hp, 0) != hipSuccess) {
+      if (hp) (void)hipHostFree(hp);
+      sh_destroy(s);
+      return fail(-ENOMEM, "hipHostMalloc (bail report) failed");
+    }
+    s->bail_host = static_cast<uint32_t*>(hp);
+    *s->bail_host = 0;
+  }
   if (cfg->schedule == RAFT_SCHED_ALIGNED) {
     if ((rc = dalloc(s, &d.skey, s->C)) || (rc = dalloc(s, &d.shist, rs::SCHED_BUCKETS)) ||
         (rc = dalloc(s, &s->soff, rs::SCHED_BUCKETS)) ||
@@ -274,7 +306,10 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       // histogram come from the previous tick launch, or are recomputed from the state. With
       // RS_RESORT_EVERY = k > 1 the packing is rebuilt every k-th launch and reused in between
       // (any packing gives the same results); only the launch before a rebuild writes keys.
-      if (s->resort_ctr % RS_RESORT_EVERY == 0) {
+      auto every = [&](uint64_t ctr) -> uint64_t {
+        return s->d.lite && ctr >= 8 ? RS_RESORT_EVERY_LITE : RS_RESORT_EVERY;
+      };
+      if (s->resort_ctr % every(s->resort_ctr) == 0) {
         if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
         HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream));
         // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
@@ -284,7 +319,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
         s->keys_fresh = true;
       }
       ++s->resort_ctr;
-      if (s->resort_ctr % RS_RESORT_EVERY != 0) {   // no rebuild after this launch: no keys
+      if (s->resort_ctr % every(s->resort_ctr) != 0) {   // no rebuild after this launch: no keys
         keep_hist = s->d.shist;
         s->d.shist = nullptr;
       }
@@ -298,7 +333,19 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
                           (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
 #endif
-    const bool steady = s->steady_ok && s->d.lite;   // host writes may have cleared lite
+    bool steady = s->steady_ok && s->d.lite;   // host writes may have cleared lite
+    if (steady && s->steady_mode == 2) steady = false;
+    if (steady && s->steady_mode == 0) {
+      if (s->steady_cooldown) {
+        --s->steady_cooldown;
+        steady = false;
+      } else if (__atomic_load_n(s->bail_host, __ATOMIC_RELAXED) > s->C / 16) {
+        __atomic_store_n(s->bail_host, 0u, __ATOMIC_RELAXED);
+        s->steady_cooldown = STEADY_COOLDOWN - 1;
+        steady = false;
+      }
+    }
+    s->last_steady = steady;
     if (steady) {
       s->d.nbail = s->nbail2 + s->steady_parity;
       s->d.nbail_zero = s->nbail2 + (s->steady_parity ^ 1);
@@ -936,6 +983,24 @@ int raft_sim_read_counters(raft_sim_t* r, raft_counters_t* out) {
   }
   return 0;
 }
+
+// Diagnostic (not part of include/raftsim.h): clusters the steady kernel handed to the catch-up
+// launch in the handle's last tick launch, summed over shards; -1 if that launch did not take the
+// steady path (tests use it to check which path ran; results never depend on it).
+extern "C" int raftsim_diag_last_bails(raft_sim_t* r) {
+  if (!r) return fail(-EINVAL, "null sim");
+  int total = 0;
+  for (Shard* s : r->sh) {
+    if (!s->steady_ok || !s->last_steady) return -1;
+    uint32_t v = 0;
+    HIP_OK(hipSetDevice(s->cfg.device));
+    HIP_OK(hipStreamSynchronize(s->stream));
+    HIP_OK(hipMemcpy(&v, s->nbail2 + (s->steady_parity ^ 1), 4, hipMemcpyDeviceToHost));
+    total += (int)v;
+  }
+  return total;
+}
+
 
 #if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
 // Diagnostic builds only (not part of include/raftsim.h): the per-wave timeline of shard 0's last

@@ -31,26 +31,38 @@ namespace rs {
 
 constexpr int SCW = 4;   // words per pair cell: arrival, term, a, b | hdr << 24 (free: word 3 == 0)
 
+// clusters per wave (whole clusters, one lane per node)
 template <int N>
-constexpr int steady_cells() { return (64 / N) * N * (N - 1); }
+constexpr int steady_cpw() { return 64 / N; }
+// words of pad after each cluster's cells (spreads the clusters' cells over the LDS banks)
+#ifndef RS_CPAD
+#define RS_CPAD 0
+#endif
+template <int N>
+constexpr int steady_cluster_words() { return N * (N - 1) * SCW + RS_CPAD; }
+template <int N>
+constexpr int steady_cell_words() { return steady_cpw<N>() * steady_cluster_words<N>(); }
 template <int N>
 constexpr size_t steady_lds_bytes() {
-  return (size_t)(steady_cells<N>() * SCW + (64 / N) * 2 * N + LCTR_WORDS) * sizeof(uint32_t);
+  return (size_t)(steady_cell_words<N>() + steady_cpw<N>() * 2 * N + LCTR_WORDS) * sizeof(uint32_t);
 }
 
 // fl bits kept beside the packed flags word (pack_flags) while the kernel runs
 constexpr uint32_t SF_ACKBAD = 1u << 15;   // log_len > checker hwm: a success response is a check
+// every queued message of the REQ (RES) list has the head's arrival, so a pop knows the next head's
+// arrival without reading its cell (messages delivered in one tick share their arrival)
+constexpr uint32_t SF_REQSAME = 1u << 16, SF_RESSAME = 1u << 17;
 
 template <int N>
 __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   static_assert(N >= 2 && N <= 5, "4-bit sender lists of at most four entries");
-  constexpr int CPW = 64 / N;
+  constexpr int CPW = steady_cpw<N>();
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* const cells = smem;                                   // [CPW*N][N-1][SCW]
-  int32_t* const rows = reinterpret_cast<int32_t*>(smem + steady_cells<N>() * SCW);  // [CPW][2N]
-  uint32_t* const lctr = smem + steady_cells<N>() * SCW + CPW * 2 * N;
+  uint32_t* const cells = smem;                      // [CPW][N][N-1][SCW] (+ pad per cluster)
+  int32_t* const rows = reinterpret_cast<int32_t*>(smem + steady_cell_words<N>());  // [CPW][2N]
+  uint32_t* const lctr = smem + steady_cell_words<N>() + CPW * 2 * N;
   const int lane = threadIdx.x;
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
   if (blockIdx.x == 0 && lane == 0) *S.nbail_zero = 0;   // the bail counter of the next launch
@@ -59,23 +71,24 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
   const uint32_t nslots = S.perm ? *S.nslots : S.C;
   if (wave * CPW >= nslots) return;
   const int cs = lane / N, k = lane - cs * N;
+  const int bl = (cs < CPW ? cs : 0) * N;
   const uint32_t slot = wave * CPW + cs;
-  const uint32_t c0 = lane < CPW * N && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
+  const uint32_t c0 = cs < CPW && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
   const bool active = c0 != INF;
   const uint32_t c = active ? c0 : 0u;
   const uint32_t g = S.goff + c, gi = c * N + k, id = k + 1;
-  const int bl = (cs < CPW ? cs : 0) * N;
   const uint32_t peers = ALL & ~(1u << id);
   const uint32_t cmask = (1u << N) - 1;
   uint32_t* const hp = S.hot + (size_t)c * HB + k;
   uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
-  int32_t* const myrows = rows + cs * 2 * N;                     // next[N], then match[N]
+  int32_t* const myrows = rows + (cs < CPW ? cs : 0) * 2 * N;    // next[N], then match[N]
   // this lane's pair cells: outgoing (to receiver index j) and incoming (from sender index s)
-  auto cell_out = [&](int j) { return cells + ((bl + k) * (N - 1) + (j < k ? j : j - 1)) * SCW; };
-  auto cell_in = [&](int s) { return cells + ((bl + s) * (N - 1) + (k < s ? k : k - 1)) * SCW; };
-  if (lane < CPW * N) {            // every pair cell starts free
+  uint32_t* const ccells = cells + (cs < CPW ? cs : 0) * steady_cluster_words<N>();
+  auto cell_out = [&](int j) { return ccells + (k * (N - 1) + (j < k ? j : j - 1)) * SCW; };
+  auto cell_in = [&](int s) { return ccells + (s * (N - 1) + (k < s ? k : k - 1)) * SCW; };
+  if (cs < CPW) {                  // every pair cell starts free
 #pragma unroll
-    for (int j = 0; j < N - 1; ++j) cells[(lane * (N - 1) + j) * SCW + 3] = 0;
+    for (int j = 0; j < N - 1; ++j) ccells[(k * (N - 1) + j) * SCW + 3] = 0;
   }
   __builtin_amdgcn_wave_barrier();
 
@@ -87,6 +100,19 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
     return m;
   };
 
+#ifdef RS_WAVELOG   // diagnostic build: per-wave timeline + per-phase cycles (scripts/wavelog_probe.py)
+  const uint64_t wl_start = wall_clock64();
+  uint32_t wl_trips = 0, wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t wl_ts = __builtin_amdgcn_s_memtime();
+#define RS_PHASE(i)                                          \
+  do {                                                       \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+    wl_ph[i] += (uint32_t)(now_ - wl_ts);                    \
+    wl_ts = now_;                                            \
+  } while (0)
+#else
+#define RS_PHASE(i) do {} while (0)
+#endif
   // ------------------------------------------------------------------ state load (launch start)
   uint32_t fl = 0, mk = 0, term = 0, commit = 0, len = 0, deadline = INF, rqa = INF, rsa = INF;
   uint32_t lists = 0;             // REQ senders (id) in nibbles 0-3, RES senders in nibbles 4-7
@@ -140,6 +166,7 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
   bool run = wb;                            // the cluster still runs here (not bailed)
   __builtin_amdgcn_wave_barrier();
 
+  RS_PHASE(9);
   const uint32_t tend = t0 + nt, d = S.dmin;
   uint32_t tnext = t0;
   for (;;) {
@@ -148,6 +175,10 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
     t = t < tend ? t : tend;
     const bool on = run && t < tend;
     if (!__ballot(on)) break;
+#ifdef RS_WAVELOG
+    ++wl_trips;
+#endif
+    RS_PHASE(8);
     const bool live = on && !((fl >> 10) & 7);
     const uint32_t role = fl & 3;
     const bool rqok = live && rqa <= t, rsok = live && rsa <= t;
@@ -170,7 +201,8 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
       if (which < 0) {
         // heartbeat: leader with full leader-state, no LazySeq log, commit within the log (the
         // IOOBE/NPE/CCE checks of append-entries-rpc pass), an empty broadcast (every peer's
-        // prev-index at or past the log's end) and every outgoing cell free
+        // prev-index at or past the log's end) and every outgoing cell free. The row and cell
+        // reads are independent (all in flight at once).
         ok = role == RAFT_LEADER && ((fl >> 14) & 1) && (keys & peers) == peers &&
              !((fl >> 13) & 1) && commit <= len;
 #pragma unroll
@@ -201,6 +233,7 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
       run = false;
       continue;
     }
+    RS_PHASE(3);
     // ------------------------------------------------ run the event
     uint32_t sent = 0;             // receivers (bits 1..N); bit 31: replies (RES queues)
     if (ev) {
@@ -210,7 +243,8 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
         const int sh = which ? 16 : 0;
         const uint32_t rest = ((lists >> sh) & 0xFFFFu) >> 4;
         lists = (lists & ~(0xFFFFu << sh)) | rest << sh;
-        const uint32_t na = rest ? cell_in((int)(rest & 15) - 1)[0] : INF;
+        const uint32_t same = fl & (which ? SF_RESSAME : SF_REQSAME);
+        const uint32_t na = !rest ? INF : same ? (which ? rsa : rqa) : cell_in((int)(rest & 15) - 1)[0];
         if (which) rsa = na;
         else rqa = na;
         tsrc = src;
@@ -222,9 +256,9 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
         for (int j = 0; j < N; ++j) {
           if (j == k) continue;
           const int32_t nx = myrows[j];
-          const uint32_t prev = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
+          const uint32_t pv = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
           *reinterpret_cast<uint4*>(cell_out(j)) =
-              make_uint4(t + d, term, commit, prev | (RAFT_MSG_APPEND_ENTRIES | id << 3) << 24);
+              make_uint4(t + d, term, commit, pv | (RAFT_MSG_APPEND_ENTRIES | id << 3) << 24);
         }
         sent = peers;
         lctr_add(lctr, RAFT_CTR_SENT, N - 1);
@@ -259,6 +293,7 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
       trace = trace_event(trace, t, evc, tsrc, tterm, r2, term, 0);
       lctr_add(lctr, RAFT_CTR_EV_RV + evc - 1, 1);
     }
+    RS_PHASE(4);
     // ------------------------------------------------ P2: deliveries, in sender id order
     if (__ballot(sent != 0)) {
       uint32_t inm = 0, rep = 0;
@@ -283,16 +318,77 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
           cell_in(j)[3] = 0;
         } else {
           lists |= (uint32_t)(j + 1) << (sh + 4 * cnt);
+          const uint32_t sb = sh ? SF_RESSAME : SF_REQSAME;
           if (!cnt) {
+            fl |= sb;
             if (sh) rsa = t + d;
             else rqa = t + d;
+          } else if ((sh ? rsa : rqa) != t + d) {
+            fl &= ~sb;
           }
           lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
         }
       }
     }
+    RS_PHASE(5);
+    // ------------------------------------------------ the leader's append-response drain
+    // Ticks at which the cluster's only event is an append-response at its row owner (the leader)
+    // run here, one response per tick as above, without the cluster's trip: up to the cluster's
+    // next other event E (every other node's next event and the leader's REQ head), the leader's
+    // heartbeat tick, or a response outside the model (the trip then decides it).
+    const bool drl = on && lsp && (fl & (3u | 7u << 10)) == RAFT_LEADER && (lists >> 16) != 0;
+    if (__ballot(drl)) {
+      const uint32_t oth = !on || ((fl >> 10) & 7) ? INF : drl ? rqa : min(deadline, min(rqa, rsa));
+      const uint32_t E = min(cluster_min(oth), tend);
+      uint32_t tl = t;
+      if (drl) {
+        for (;;) {
+          const uint32_t tau = max(min(rsa, deadline), tl + 1);
+          if (tau >= E || rsa > tau) break;
+          const int hs = (int)((lists >> 16) & 15) - 1;
+          const uint4 x = *reinterpret_cast<const uint4*>(cell_in(hs));
+          const uint32_t xh = x.w >> 24, xf = (xh >> 7) & 1, xs = (uint32_t)hs + 1;
+          if ((xh & 7) != RAFT_MSG_APPEND_RESPONSE || x.y > term ||
+              (xf ? (fl & SF_ACKBAD) != 0 : ((mk >> (16 + xs)) & 1) == 0))
+            break;
+          cell_in(hs)[3] = 0;
+          const uint32_t rest = (lists >> 20) & 0xFFFu;
+          lists = (lists & 0xFFFFu) | rest << 16;
+          rsa = !rest ? INF : (fl & SF_RESSAME) ? rsa : cell_in((int)(rest & 15) - 1)[0];
+          if (xf) {
+            mk |= 1u << (16 + xs);
+            myrows[hs] = (int32_t)(x.w & 0xFFFFFFu);
+            myrows[N + hs] = (int32_t)x.z;
+          } else {
+            myrows[hs] -= 1;
+          }
+          deadline = tau + S.hb;
+          trace = trace_event(trace, tau, RAFT_MSG_APPEND_RESPONSE, xs, x.y, RAFT_LEADER, term, 0);
+          lctr_add(lctr, RAFT_CTR_EV_AR, 1);
+          tl = tau;
+        }
+      }
+      if (lspm) t = max(t, __shfl(tl, bl + __builtin_ctz(lspm)));   // the cluster takes its clock
+    }
+    RS_PHASE(6);
     tnext = t + 1;
   }
+#ifdef RS_WAVELOG
+  if (lane == 0 && S.wavelog) {
+    const uint64_t wl_end = wall_clock64();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 32);
+    rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
+                        (uint32_t)(wl_end >> 32));
+    rec[1] = make_uint4(wl_trips, hw, xcc, 0);
+    rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
+    rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
+    rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
+    rec[5] = make_uint4(0, 0, 0, 0);
+  }
+#endif
 
   // ------------------------------------------------------------------ write back
   if (S.shist) {
@@ -312,7 +408,7 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
     }
   }
   if (wb) {
-    hp[HF_FLAGS * N] = fl & ~SF_ACKBAD;
+    hp[HF_FLAGS * N] = fl & 0x7FFFu;
     hp[HF_MASKS * N] = mk;
     hp[HF_TERM * N] = term; hp[HF_COMMIT * N] = commit; hp[HF_DEADLINE * N] = deadline;
     hp[HF_TRACE_LO * N] = (uint32_t)trace; hp[HF_TRACE_HI * N] = (uint32_t)(trace >> 32);
@@ -350,13 +446,15 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
 }
 
 // The steady kernel for N <= 5 (LITE launches; the caller checks). Grid: the packing's slots.
-hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, uint32_t waves, hipStream_t st,
+hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0) {
+  const uint32_t slots = S.perm ? sched_slots_bound(S.C, S.N) : S.C;
   switch (S.N) {
 #define RS_STEADY(NN)                                                                            \
   case NN:                                                                                       \
-    hipExtLaunchKernelGGL((steady_kernel<NN>), dim3(waves), dim3(64), steady_lds_bytes<NN>(), st, \
-                          ev0, nullptr, 0, S, t0, nt);                                          \
+    hipExtLaunchKernelGGL((steady_kernel<NN>),                                                   \
+                          dim3((slots + steady_cpw<NN>() - 1) / steady_cpw<NN>()), dim3(64),     \
+                          steady_lds_bytes<NN>(), st, ev0, nullptr, 0, S, t0, nt);              \
     break;
     RS_STEADY(2) RS_STEADY(3) RS_STEADY(4) RS_STEADY(5)
 #undef RS_STEADY

@@ -433,6 +433,7 @@ tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   // waves take wave slots wave, wave + gridDim.x, ... in turn.
   const uint32_t nslots = S.perm ? *S.nslots : S.C;
   uint32_t wave = blockIdx.x;
+  if (CATCH && wave == 0 && lane == 0 && S.bail_report) *S.bail_report = nslots;
   if (wave * CPW >= nslots) return;
   do {
     if (CATCH) tripsL[lane] = 0;
@@ -1740,11 +1741,16 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
 #ifndef RS_KERNEL_ONLY   // scripts/quick_vgpr.sh compiles one instantiation without the launchers
 // The tick kernel's own start/stop timestamps go into ev0/ev1 through its dispatch packet
 // (hipExtLaunchKernelGGL): no marker packets between launches (each cost ~5.7 us of idle GPU).
-hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, uint32_t waves, hipStream_t st,
+hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0);
 
-// Catch-up waves: at most one per SIMD; each takes wave slots in turn (tick_kernel<..., CATCH>).
-constexpr uint32_t CATCH_WAVES = 1024;
+// Catch-up waves: each takes wave slots in turn (tick_kernel<..., CATCH>). Few, so that an empty
+// catch-up launch costs little (the host falls back to the general kernel while many clusters
+// bail: raftsim.hip, steady_mode).
+#ifndef RS_CATCH_WAVES
+#define RS_CATCH_WAVES 256
+#endif
+constexpr uint32_t CATCH_WAVES = RS_CATCH_WAVES;
 
 template <int N, bool SPEC>
 hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
@@ -1756,7 +1762,7 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
     if (steady) {
       // steady kernel over every cluster, then the general kernel over the clusters it bailed,
       // each from the tick it stopped before; the launch's timing spans both
-      const hipError_t e = launch_steady(S, t0, nt, waves, st, ev0);
+      const hipError_t e = launch_steady(S, t0, nt, st, ev0);
       if (e != hipSuccess) return e;
       DevSim B = S;
       B.perm = S.bail_c;

@@ -24,3 +24,13 @@ class Simulator(Backend):
         if not LIB_PATH.exists():
             raise RaftSimError(f"{LIB_PATH} not built: run __graft_entry__.build()")
         super().__init__(LIB_PATH, "raft_sim_", **config)
+
+    def diag_last_bails(self):
+        """Diagnostic: clusters the steady kernel handed to the general kernel in the last tick
+        launch (steady_kernel.hip), or -1 if that launch did not take the steady path."""
+        import ctypes
+
+        f = self._lib.raftsim_diag_last_bails
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p]
+        return int(f(self._h))

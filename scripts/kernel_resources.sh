@@ -6,11 +6,14 @@ set -e
 TAG=${1:-r12}
 R=$(cd "$(dirname "$0")/.." && pwd)
 S=$(mktemp /tmp/tick_kernel_XXXX.s)
+S2=$(mktemp /tmp/steady_kernel_XXXX.s)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -S --cuda-device-only -o $S \
   $R/raft-simulation_amd/csrc/tick_kernel.hip 2>/dev/null
-python3 - "$S" > $R/profiles/${TAG}_kernel_resources.txt <<'PY'
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -S --cuda-device-only -o $S2 \
+  $R/raft-simulation_amd/csrc/steady_kernel.hip 2>/dev/null
+python3 - "$S" "$S2" > $R/profiles/${TAG}_kernel_resources.txt <<'PY'
 import re, sys
-s = open(sys.argv[1]).read()
+s = open(sys.argv[1]).read() + open(sys.argv[2]).read()
 print(f"{'kernel':48s} {'VGPRs':>5s} {'SGPRs':>5s} {'scratch':>7s} {'waves/SIMD':>10s}")
 for m in re.finditer(r'^(_ZN2rs\w+):\s', s, re.M):
     name = m.group(1)
@@ -18,11 +21,14 @@ for m in re.finditer(r'^(_ZN2rs\w+):\s', s, re.M):
     tail = s[s.index('.Lfunc_end', m.end()):][:4000]
     get = lambda k: (re.search(r'; ' + k + r': (\d+)', tail) or [None, '?'])[1]
     pretty = name.replace('_ZN2rs', 'rs::')
-    mt = re.match(r'rs::11tick_kernelILi(\d)ELb(\d)ELb(\d)ELb(\d)', pretty)
+    mt = re.match(r'rs::11tick_kernelILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)', pretty)
     if mt:
         pretty = (f"tick_kernel<N={mt.group(1)}, TRACE={mt.group(2)}, SPEC={mt.group(3)}, "
-                  f"LITE={mt.group(4)}>")
+                  f"LITE={mt.group(4)}{', CATCH' if mt.group(5) == '1' else ''}>")
+    ms = re.match(r'rs::13steady_kernelILi(\d)E', pretty)
+    if ms:
+        pretty = f"steady_kernel<N={ms.group(1)}>"
     print(f"{pretty[:48]:48s} {get('NumVgprs'):>5s} {get('TotalNumSgprs'):>5s} {get('ScratchSize'):>7s} {get('Occupancy'):>10s}")
 PY
-rm -f $S
+rm -f $S $S2
 cat $R/profiles/${TAG}_kernel_resources.txt

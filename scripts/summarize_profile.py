@@ -27,6 +27,23 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 KERNEL = "tick_kernel"
+STEADY = "steady_kernel"        # LITE launches: the steady kernel, then the catch-up tick kernel
+
+
+def launch_groups(rows, name_key):
+    """Group dispatch-ordered rows into tick launches: a steady_kernel dispatch together with the
+    catch-up tick_kernel dispatch that follows it, or one tick_kernel dispatch."""
+    groups = []
+    for r in rows:
+        nm = r[name_key]
+        if STEADY in nm:
+            groups.append([r])
+        elif KERNEL in nm:
+            if groups and len(groups[-1]) == 1 and STEADY in groups[-1][0][name_key]:
+                groups[-1].append(r)
+            else:
+                groups.append([r])
+    return groups
 
 
 def counters_by_kernel(path):
@@ -83,19 +100,30 @@ def main():
         d = src / f"pmc{i}"
         if not d.exists():
             continue
-        for kname, vals in counters_by_kernel(d).items():
-            if KERNEL in kname:
-                for c, v in vals.items():
-                    pmc[c].extend(v)
+        rows = []
+        for f in sorted(d.glob("**/*counter_collection.csv")):
+            rows.extend(csv.DictReader(open(f)))
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id") or 0))
+        # one value per counter per dispatch, then summed over each launch's dispatches
+        disp = collections.OrderedDict()
+        for r in rows:
+            if KERNEL in r["Kernel_Name"] or STEADY in r["Kernel_Name"]:
+                e = disp.setdefault(r["Dispatch_Id"], {"Kernel_Name": r["Kernel_Name"], "c": {}})
+                e["c"][r["Counter_Name"]] = e["c"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for g in launch_groups(list(disp.values()), "Kernel_Name"):
+            for c in g[0]["c"]:
+                pmc[c].append(sum(x["c"].get(c, 0.0) for x in g))
     # the timed launches only: the last `launches` dispatches of the tick kernel (warm-up
     # launches, on the same or a throwaway handle, come first)
     nl = max(1, bench["roofline"]["launches"])
     avg = {k: sum(v[-nl:]) / len(v[-nl:]) for k, v in pmc.items()}
     trace = list(csv.DictReader(open(src / "kt" / "run_kernel_trace.csv")))
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
-            if KERNEL in r["Kernel_Name"]]
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # a launch spans its dispatches (steady kernel start to catch-up end), as the HIP events do
+    groups = launch_groups(trace, "Kernel_Name")
+    durs = [int(g[-1]["End_Timestamp"]) - int(g[0]["Start_Timestamp"]) for g in groups]
     stats = [r for r in csv.DictReader(open(src / "kt" / "run_kernel_stats.csv"))
-             if KERNEL in r["Name"]]
+             if KERNEL in r["Name"] or STEADY in r["Name"]]
     durs = durs[-max(1, bench["roofline"]["launches"]):]   # the timed launches, not the warm-up
     avg_ns = sum(durs) / max(1, len(durs))
 
@@ -119,14 +147,18 @@ def main():
     achieved = event_bytes / (avg_ns * 1e-9) / 1e9
     out = {
         "tag": tag, "workload": wl, "kernel_src_sha": roof["kernel_src_sha"],
-        "kernel": next((r["Kernel_Name"] for r in trace if KERNEL in r["Kernel_Name"]), None),
+        "kernel": [r["Kernel_Name"] for r in groups[-1]] if groups else None,
         "launches_traced": len(durs), "avg_duration_ns_trace": avg_ns,
-        "avg_duration_ns_stats": float(stats[0]["AverageNs"]) if stats else None,
+        "avg_duration_ns_per_kernel_stats": {r["Name"]: float(r["AverageNs"]) for r in stats},
+        "launch_note": "a LITE launch is the steady kernel then the catch-up tick kernel; its "
+                       "duration runs from the first dispatch's start to the last one's end "
+                       "(the span the bench's HIP events time) and its PMC counts are the sum "
+                       "over both dispatches",
         "bench_avg_launch_ms_hip_events": roof["avg_launch_ms"],
         # rocprofv3's VGPR_Count field is the allocation granule count of another encoding; the
         # compiler's own register count is in profiles/TAG_kernel_resources.txt
-        "vgpr_rocprof_field": next((r.get("VGPR_Count") for r in trace
-                                    if KERNEL in r["Kernel_Name"]), None),
+        "vgpr_rocprof_field": {r["Kernel_Name"]: r.get("VGPR_Count") for r in groups[-1]}
+        if groups else None,
         "vgpr_compiler": vgpr_compiler(tag, n),
         "pmc_per_launch": avg,
         # occupancy (MI355X_MICROARCH.md: SQ_WAVE_CYCLES in quad-cycles summed over waves;

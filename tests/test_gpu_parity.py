@@ -80,6 +80,21 @@ CASES = {
     "redirect_storm": dict(n_clusters=512, nodes=6, seed=65, client_ppm=1000000,
                            client_period=300, client_burst=40, client_redirects=16, inbox_cap=4,
                            log_cap=128, hb=50, el_base=80, el_span=80, **FAULTS),
+    # LITE launches (no faults, no client, fixed delay) at N <= 5 take the steady kernel and hand
+    # every other event to the catch-up launch (steady_kernel.hip): its edges
+    "lite_n2": dict(n_clusters=1000, nodes=2, seed=71, hb=40, el_base=60, el_span=40),
+    "lite_n3": dict(n_clusters=1000, nodes=3, seed=73, hb=300, el_base=500, el_span=500),
+    "lite_n4": dict(n_clusters=1000, nodes=4, seed=75, hb=300, el_base=500, el_span=500, dmin=4,
+                    dmax=4),
+    # heartbeats slower than the election timer: elections keep interrupting the rounds
+    "lite_elections": dict(n_clusters=1200, nodes=5, seed=77, hb=700, el_base=500, el_span=400,
+                           dmin=3, dmax=3),
+    # two-slot inboxes: a leader's four responses overflow its RES ring (the slow delivery path)
+    "lite_tiny_inbox": dict(n_clusters=1200, nodes=5, seed=79, inbox_cap=2, hb=200, el_base=500,
+                            el_span=300),
+    # odd launch splits: queued messages cross launch boundaries into the pair cells
+    "lite_odd_launches": dict(n_clusters=600, nodes=5, seed=81, ticks_per_launch=13, hb=60,
+                              el_base=100, el_span=100, dmin=7, dmax=7),
 }
 
 
@@ -334,3 +349,37 @@ def test_gpu_c3_full_size_sampled(variant):
         r.step(10000)
         bad = np.nonzero(g.digest(lo, part) != r.digest())[0]
         assert not len(bad), f"{len(bad)} clusters of [{lo}, {lo + part}) differ; first {lo + bad[0]}"
+
+
+def test_gpu_steady_path_taken():
+    """C2 from init-node: the first launch (every cluster still has to elect) takes the general
+    kernel (-1); once every cluster has its leader the steady kernel runs every cluster alone
+    (0 bails); the state equals the oracle's after every launch."""
+    cfg = dict(n_clusters=8192, nodes=5, seed=83)
+    g = helpers.gpu(**cfg)
+    r = helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    bails = []
+    for _ in range(4):
+        g.step(10000)
+        r.step(10000)
+        bails.append(g.diag_last_bails())
+        assert (g.digest() == r.digest()).all()
+    assert g.counters() == r.counters()
+    assert bails[0] == -1 and bails[-1] == 0, bails
+
+
+LITE_CASES = ["c2_small", "lite_n2", "lite_n3", "lite_n4", "lite_elections", "lite_tiny_inbox",
+              "lite_odd_launches"]
+
+
+@pytest.mark.parametrize("name", LITE_CASES)
+def test_gpu_forced_steady_matches_oracle(name, monkeypatch):
+    """Every LITE launch on the steady kernel (RAFTSIM_STEADY=always), from init-node: elections
+    and every other event outside its model go through the catch-up launch, whose waves take
+    several wave slots each; GPU == oracle after every chunk."""
+    monkeypatch.setenv("RAFTSIM_STEADY", "always")
+    cfg = CASES[name]
+    g, r = run_pair(cfg, 20000, 5000)
+    assert g.counters() == r.counters()
+    assert g.diag_last_bails() >= 0          # the last launch took the steady path
