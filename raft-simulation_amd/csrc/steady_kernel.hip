@@ -445,10 +445,610 @@ __global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint3
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lane-per-cluster form of the steady kernel. One lane runs one whole cluster: the leader and its
+// N-1 followers are named registers (follower slot j is the j-th non-leader node in id order), the
+// messages in flight are registers too (a follower holds at most one append-entries from the
+// leader; the leader's append-responses all share one arrival and pop in sender id order), and no
+// event needs another lane: no shuffles, ballots or LDS inside the tick loop, and a wave runs 64
+// clusters instead of 12. The events and their order are the steady kernel's (heartbeat-handler,
+// append-entries-handler and append-response-handler of core.clj:105-164, SIM_SPEC.md §4), and any
+// cluster outside this narrower model (no single leader with full leader-state, a halted node, a
+// message of another shape, a follower timing out, a response of a newer term, ...) is bailed
+// before that tick exactly as above, so results are the general kernel's for any state.
+// Grid: 256-thread workgroups, one cluster per thread, slots in the packing's order (clusters with
+// the same next event share a wave, so lanes take the same branch on every trip).
+constexpr int LANE_WG = 256;
+// clusters per wave: 64, or 32 (half the lanes idle, twice the waves: two per SIMD hide each
+// other's dependency latency)
+#ifndef RS_LANE_CPW
+#define RS_LANE_CPW 64
+#endif
+constexpr int LANE_CPW = RS_LANE_CPW;
+constexpr int LANE_CPB = LANE_WG / 64 * LANE_CPW;   // clusters per workgroup
+#ifndef RS_LANE_STAGE
+#define RS_LANE_STAGE 1
+#endif
+// words of each cluster block staged through LDS: fields FLAGS..TRACE_HI, whole lines
+__host__ __device__ constexpr int lane_stage_words(int N) { return (HF_NEXT * N + 31) / 32 * 32; }
+__host__ __device__ constexpr size_t lane_lds_bytes(int N) {
+  return RS_LANE_STAGE ? (size_t)(LANE_WG / 64) * LANE_CPW * (lane_stage_words(N) + 1) * 4 : 0;
+}
+#ifndef RS_STEADY_LANE
+#define RS_STEADY_LANE 1
+#endif
+#ifndef RS_LANE_DRAIN
+#define RS_LANE_DRAIN 1
+#endif
+
+// v = vals[k] for a runtime k < N, as masks (a select chain over an array is turned back into an
+// indexed load from memory by the compiler; this keeps the array in registers)
+template <int N>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&vals)[N], uint32_t k) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v |= vals[i] & (0u - (uint32_t)(k == (uint32_t)i));
+  return v;
+}
+// a ? x : y without a select the compiler could fold into an indexed load
+__device__ __forceinline__ uint32_t msel(bool a, uint32_t x, uint32_t y) {
+  const uint32_t m = 0u - (uint32_t)a;
+  return (x & m) | (y & ~m);
+}
+
+template <int N>
+__global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+  static_assert(N >= 2 && N <= 5, "follower masks and the response queue fit four followers");
+  constexpr int F = N - 1;
+  constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
+  constexpr int NW4 = (int)(CLW + 4) / 4;          // uint4s up to and including the checker hwm
+  __shared__ uint32_t sctr[4];
+  const uint32_t nslots = S.perm ? *S.nslots : S.C;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *S.nbail_zero = 0;   // the next launch's bail counter
+  if (blockIdx.x * LANE_CPB >= nslots) return;                  // workgroup-uniform
+  if (threadIdx.x < 4) sctr[threadIdx.x] = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t slot = blockIdx.x * LANE_CPB + threadIdx.x / 64 * LANE_CPW + lane;
+  const uint32_t c0 = lane < (uint32_t)LANE_CPW && slot < nslots ? (S.perm ? S.perm[slot] : slot)
+                                                                 : INF;
+  const bool active = c0 != INF;
+  const uint32_t c = active ? c0 : 0u;
+  const uint32_t g = S.goff + c;
+  uint32_t* const blk = S.hot + (size_t)c * HB;
+#ifdef RS_WAVELOG   // diagnostic build: per-wave timeline (scripts/lane_timeline.py)
+  const uint64_t wl_start = wall_clock64();
+  uint32_t wl_trips = 0, wl_first = 0;
+  uint64_t wl_loop = 0;
+#endif
+
+  // ------------------------------------------- load: fields FLAGS..RES_ARR, TRACE, checker hwm
+  uint32_t w[NW4 * 4];
+#pragma unroll
+  for (int i = 0; i < NW4 * 4; ++i) w[i] = 0;
+#if RS_LANE_STAGE
+  // The first LW words of every block (fields FLAGS..TRACE_HI and the first rows) go through the
+  // wave's LDS tile: whole 128-B lines, eight per load instruction, instead of one 16-B piece of
+  // 64 different lines per instruction (a request per lane: the load and write-back phases were
+  // bound by L2 request rate, not bytes). Row stride LW + 1 (odd): lanes reading the same word of
+  // their own rows hit distinct banks.
+  constexpr int LW = lane_stage_words(N), SW = LW + 1, U4 = LW / 4;
+  extern __shared__ uint32_t lsm[];
+  uint32_t* const tile = lsm + (threadIdx.x / 64) * (LANE_CPW * SW);
+  uint32_t* const myrow = tile + (lane < (uint32_t)LANE_CPW ? lane : 0) * SW;
+  {
+    const uint32_t cc = active ? c : INF;
+#pragma unroll
+    for (int i = 0; i < LANE_CPW * U4 / 64; ++i) {
+      const uint32_t x = i * 64 + lane, b = x / U4, u = x - b * U4;
+      const uint32_t cb = (uint32_t)__shfl((int)cc, (int)b);
+      if (cb != INF) {
+        const uint4 v = reinterpret_cast<const uint4*>(S.hot + (size_t)cb * HB)[u];
+        uint32_t* r = tile + b * SW + 4 * u;
+        r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+      }
+    }
+  }
+  __syncthreads();
+  if (active) {
+#pragma unroll
+    for (int q = 0; q < (int)(HF_NEXT * N); ++q) w[q] = myrow[q];
+    w[CLW] = blk[CLW];
+  }
+#else
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < NW4; ++i) {
+      const int lo = 4 * i, hi = 4 * i + 3;
+      const bool need = lo < (int)(HF_REQ_TAIL * N) ||
+                        (hi >= (int)(HF_TRACE_LO * N) && lo < (int)(HF_NEXT * N)) ||
+                        (lo <= (int)CLW && hi >= (int)CLW);
+      if (need) {
+        const uint4 x = reinterpret_cast<const uint4*>(blk)[i];
+        w[lo] = x.x; w[lo + 1] = x.y; w[lo + 2] = x.z; w[lo + 3] = x.w;
+      }
+    }
+  }
+#endif
+  auto field = [&](int f, uint32_t (&out)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = w[f * N + k];
+  };
+  uint32_t nfl[N], nqm[N];
+  field(HF_FLAGS, nfl);
+  field(HF_QMETA, nqm);
+  // exactly one leader; every node running; only the leader has leader-state
+  uint32_t L = 0, nlead = 0, badn = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint32_t f = nfl[k];
+    const bool lead = (f & 3) == RAFT_LEADER;
+    L = lead ? (uint32_t)k : L;
+    nlead += lead;
+    badn |= ((f >> 10) & 7) | (lead != (((f >> 14) & 1) != 0));
+  }
+  bool bad = !active || nlead != 1 || badn != 0 || S.Q < (uint32_t)F;
+  const uint32_t Lid = L + 1;
+  // follower slot j is node j (j < L) or j + 1 (j >= L)
+  auto fsel = [&](const uint32_t (&v)[N], int j) { return msel((uint32_t)j >= L, v[j + 1], v[j]); };
+  auto fk = [&](int j) { return (uint32_t)j + ((uint32_t)j >= L ? 1u : 0u); };
+
+  uint32_t tmp[N];
+  // leader registers
+  const uint32_t Lfl = pick<N>(nfl, L);
+  field(HF_MASKS, tmp); uint32_t Lmk = pick<N>(tmp, L);
+  uint32_t fmk[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) fmk[j] = fsel(tmp, j);
+  field(HF_TERM, tmp); const uint32_t Lterm = pick<N>(tmp, L);
+  uint32_t fterm[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) fterm[j] = fsel(tmp, j);
+  field(HF_COMMIT, tmp); const uint32_t Lcommit = pick<N>(tmp, L);
+  uint32_t fcommit[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) fcommit[j] = fsel(tmp, j);
+  field(HF_LEN, tmp); const uint32_t Llen = pick<N>(tmp, L);
+  uint32_t flen[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) flen[j] = fsel(tmp, j);
+  field(HF_DEADLINE, tmp); uint32_t Ldl = pick<N>(tmp, L);
+  uint32_t fdl[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) fdl[j] = fsel(tmp, j);
+  uint32_t tlo[N], thi[N];
+  field(HF_TRACE_LO, tlo);
+  field(HF_TRACE_HI, thi);
+  uint64_t Ltr = (uint64_t)pick<N>(thi, L) << 32 | pick<N>(tlo, L);
+  uint64_t ftr[F];
+  uint32_t ffl[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    ftr[j] = (uint64_t)fsel(thi, j) << 32 | fsel(tlo, j);
+    ffl[j] = fsel(nfl, j);
+  }
+  // the leader's rows for its followers: next_index / match_index of peer id fk(j) + 1
+  int32_t nx[F], mt[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    const uint32_t qn = (HF_NEXT + fk(j)) * N + L, qm = (HF_NEXT + N + fk(j)) * N + L;
+#if RS_LANE_STAGE
+    nx[j] = active ? (int32_t)(qn < (uint32_t)LW ? myrow[qn] : blk[qn]) : 0;
+    mt[j] = active ? (int32_t)(qm < (uint32_t)LW ? myrow[qm] : blk[qm]) : 0;
+#else
+    nx[j] = active ? (int32_t)blk[qn] : 0;
+    mt[j] = active ? (int32_t)blk[qm] : 0;
+#endif
+  }
+  const bool ackbad = Llen > w[CLW];          // a success response would be checker work (P4)
+  const uint32_t Lkeys = Lmk >> 16;
+  // heartbeats need full leader-state, no LazySeq log and commit within the log
+  // (append-entries-rpc's IOOBE/NPE/CCE checks, core.clj:56-67): constant over the launch
+  bad = bad || (Lkeys & (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid))) !=
+                   (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid)) ||
+        ((Lfl >> 13) & 1) || Lcommit > Llen;
+
+  // ---------------------------------------------------------------- queued messages
+  uint32_t qmask = 0, rmask = 0, resA = INF;
+  uint32_t qA[F], qT[F], qa[F], qb[F], rT[F], rA[F], rB[F], rH[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    qA[j] = INF; qT[j] = qa[j] = qb[j] = 0;
+    rT[j] = rA[j] = rB[j] = rH[j] = 0;
+  }
+  if (!bad) {
+    const uint32_t Lqm = pick<N>(nqm, L);
+    bad = (Lqm >> 4) & 31;                                   // the leader's REQ queue is empty
+    const uint32_t rsh = (Lqm >> 9) & 15, rsc = (Lqm >> 13) & 31;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      const uint32_t qm = fsel(nqm, j);
+      const uint32_t rqh = qm & 15, rqc = (qm >> 4) & 31;
+      bad = bad || rqc > 1 || ((qm >> 13) & 31) != 0;       // <= 1 request, no responses
+      if (!bad && rqc) {                                    // the leader's append-entries
+        const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, c * N + fk(j), 0) +
+                                                         rqh * qstride(S, 0));
+        const uint4 m0 = mp[0], m1 = mp[1];
+        bad = m0.y != (RAFT_MSG_APPEND_ENTRIES | Lid << 3) || m1.y || m1.z || m1.w;
+        qmask |= 1u << j;
+        qA[j] = m0.x; qT[j] = m0.z; qa[j] = m0.w; qb[j] = m1.x;
+      }
+    }
+    bad = bad || rsc > (uint32_t)F;
+    uint32_t last = 0;
+    for (uint32_t i = 0; i < rsc && !bad; ++i) {            // append-responses, sender order
+      const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, c * N + L, 1) +
+                                                       wrapq(rsh + i, S.Q) * qstride(S, 1));
+      const uint4 m0 = mp[0], m1 = mp[1];
+      const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
+      bad = (hdr & 7) != RAFT_MSG_APPEND_RESPONSE || (hdr >> 8) || m1.y || m1.z || m1.w ||
+            src <= last || src > (uint32_t)N || src == Lid || (i && m0.x != resA);
+      last = src;
+      resA = m0.x;
+      const uint32_t j = src - 1 - (src > Lid ? 1u : 0u);
+      rmask |= 1u << j;
+#pragma unroll
+      for (int jj = 0; jj < F; ++jj) {
+        if ((uint32_t)jj == j) {
+          rT[jj] = m0.z; rA[jj] = m0.w; rB[jj] = m1.x; rH[jj] = (hdr >> 7) & 1;
+        }
+      }
+    }
+    if (!rmask) resA = INF;
+  }
+  if (active && bad) {                      // outside the model from the start: bail at t0
+    const uint32_t i = atomicAdd(S.nbail, 1u);
+    S.bail_c[i] = c;
+    S.bail_t[i] = t0;
+  }
+  const bool wb = active && !bad;
+  bool run = wb;
+
+  // ---------------------------------------------------------------- the cluster's ticks
+  const uint32_t tend = t0 + nt, d = S.dmin;
+  uint32_t tn = t0, nhb = 0, nae = 0, nar = 0;
+  auto next_event = [&]() {
+    uint32_t m = min(Ldl, resA);
+#pragma unroll
+    for (int j = 0; j < F; ++j) m = min(m, min(fdl[j], qA[j]));
+    return m;
+  };
+#ifdef RS_WAVELOG
+  wl_loop = wall_clock64();
+#endif
+  for (;;) {
+    const uint32_t t = max(tn, next_event());
+    const bool on = run && t < tend;
+    if (!__builtin_amdgcn_ballot_w64(on)) break;
+#ifdef RS_WAVELOG
+    if (!wl_trips) wl_first = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(on));
+    ++wl_trips;
+#endif
+    if (!on) continue;
+    // ------------------------------------------------ decide on the pre-tick state
+    const bool lres = rmask != 0 && resA <= t;               // a message beats the deadline
+    const bool lhb = !lres && Ldl <= t;
+    uint32_t fae = 0, fto = 0;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      const bool a = qA[j] <= t;
+      fae |= (uint32_t)a << j;
+      fto |= (uint32_t)(!a && fdl[j] <= t) << j;
+    }
+    bool bail = fto != 0;                                    // a follower's election timeout
+    if (lhb) {
+      bail = bail || qmask != 0;                             // a follower still holds one
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const uint32_t pv = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
+        bail = bail || pv < Llen || pv >= (1u << 24);        // entries to ship
+      }
+    }
+    const int hs = __builtin_ctz(rmask | (1u << F));
+    uint32_t xT = 0, xA = 0, xB = 0, xH = 0;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      if (j == hs) {
+        xT = rT[j]; xA = rA[j]; xB = rB[j]; xH = rH[j];
+      }
+    }
+    const uint32_t xid = (uint32_t)hs + 1 + ((uint32_t)hs >= L ? 1u : 0u);
+    if (lres)
+      bail = bail || xT > Lterm || (xH ? ackbad : ((Lmk >> (16 + xid)) & 1) == 0);
+    if (fae) {
+      bail = bail || rmask != 0;                             // responses of two ticks
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        if ((fae >> j) & 1)
+          bail = bail || qb[j] != 0 || !(qT[j] < fterm[j] || flen[j] <= fcommit[j]);
+    }
+    if (bail) {                              // the general kernel runs this tick
+      const uint32_t i = atomicAdd(S.nbail, 1u);
+      S.bail_c[i] = c;
+      S.bail_t[i] = t;
+      run = false;
+      continue;
+    }
+    // ------------------------------------------------ run
+    uint32_t tl = t;                         // the last tick run (the drain may run more)
+    if (lhb) {                               // heartbeat-handler: empty append-entries to all
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        qA[j] = t + d; qT[j] = Lterm; qa[j] = Lcommit;
+        qb[j] = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
+      }
+      qmask = (1u << F) - 1;
+      Ldl = t + S.hb;
+      Ltr = trace_event(Ltr, t, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+      ++nhb;
+    }
+    if (lres) {                              // append-response-handler, head in sender order
+      rmask &= rmask - 1;
+      if (!rmask) resA = INF;
+      Lmk |= xH << (16 + xid);
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if (j == hs) {
+          nx[j] = xH ? (int32_t)xB : nx[j] - 1;
+          mt[j] = xH ? (int32_t)xA : mt[j];
+        }
+      }
+      Ldl = t + S.hb;
+      Ltr = trace_event(Ltr, t, RAFT_MSG_APPEND_RESPONSE, xid, xT, RAFT_LEADER, Lterm, 0);
+      ++nar;
+#if RS_LANE_DRAIN
+      // the leader's next responses, one per tick, while nothing else in the cluster is due: the
+      // followers' next events (their deadlines; their queues are empty after they answered) and
+      // the launch end; the leader's own deadline moved past them. A response outside the model
+      // ends the drain and the next trip decides it.
+      uint32_t E = tend;
+#pragma unroll
+      for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
+      for (uint32_t tau = t + 1; rmask && tau < E; ++tau) {
+        const int h2 = __builtin_ctz(rmask);
+        uint32_t yT = 0, yA = 0, yB = 0, yH = 0;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          if (j == h2) {
+            yT = rT[j]; yA = rA[j]; yB = rB[j]; yH = rH[j];
+          }
+        }
+        const uint32_t yid = (uint32_t)h2 + 1 + ((uint32_t)h2 >= L ? 1u : 0u);
+        if (yT > Lterm || (yH ? ackbad : ((Lmk >> (16 + yid)) & 1) == 0)) break;
+        rmask &= rmask - 1;
+        if (!rmask) resA = INF;
+        Lmk |= yH << (16 + yid);
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          if (j == h2) {
+            nx[j] = yH ? (int32_t)yB : nx[j] - 1;
+            mt[j] = yH ? (int32_t)yA : mt[j];
+          }
+        }
+        Ldl = tau + S.hb;
+        Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, yid, yT, RAFT_LEADER, Lterm, 0);
+        ++nar;
+        tl = tau;
+      }
+#endif
+    }
+    if (fae) {                               // append-entries-handler at each follower
+      // every follower's handler is computed and kept where it ran: the four Philox draws and
+      // trace hashes are independent chains the compiler interleaves (in a round every follower
+      // answers the same heartbeat on the same tick)
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const bool run_j = (fae >> j) & 1;
+        const uint32_t fid = fk(j) + 1;
+        const uint4 wd = event_draw(g, fid, t, S);
+        const uint32_t mterm = qT[j], rterm = fterm[j];
+        const bool ok = mterm >= fterm[j];
+        const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER |
+                                       Lid << 6
+                                 : ffl[j];
+        const uint32_t nterm = ok ? mterm : fterm[j];
+        const uint64_t ntr = trace_event(ftr[j], t, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3,
+                                         nterm, 0);
+        if (run_j) {
+          if (ok) {
+            fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
+            fmk[j] &= 0xFFFF0000u;
+          }
+          fterm[j] = nterm;
+          ffl[j] = nfl2;
+          // the response: to the leader's RES queue, in sender id order
+          rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
+          qA[j] = INF;
+          fdl[j] = t + S.el_base + __umulhi(wd.y, S.el_span);
+          ftr[j] = ntr;
+        }
+      }
+      qmask &= ~fae;
+      rmask = fae;
+      resA = t + d;
+      nae += __popc(fae);
+    }
+    tn = tl + 1;
+  }
+
+#ifdef RS_WAVELOG
+  const uint64_t wl_lend = wall_clock64();
+  const uint32_t wl_events = nhb + nae + nar;
+#endif
+  // ---------------------------------------------------------------- write back
+  if (S.shist && wb && run) {
+    // packing key for the next launch (bailed clusters get theirs from the catch-up launch)
+    const uint32_t key = sched_bucket(next_event(), tend);
+    S.skey[c] = key;
+    atomicAdd(&S.shist[key], 1u);
+  }
+  if (wb) {
+    // every word of fields FLAGS..RES_TAIL and TRACE_LO/HI, from registers (LEN unchanged)
+    constexpr int NV = 16;
+    uint32_t v[NV][N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      // node k is the leader (k == L) or follower slot k - 1 (k > L) / k (k < L)
+      const bool isL = (uint32_t)k == L;
+      const int jl = k > 0 ? k - 1 : 0, jh = k < F ? k : F - 1;
+      const bool lo = (uint32_t)k > L;
+      auto fv = [&](const uint32_t* x) { return msel(lo, x[jl], x[jh]); };
+      const uint32_t fq = (qmask >> (lo ? jl : jh)) & 1;
+      const uint32_t fqa = fv(qA);
+      const uint64_t trf = (uint64_t)msel(lo, (uint32_t)(ftr[jl] >> 32), (uint32_t)(ftr[jh] >> 32)) << 32 |
+                          msel(lo, (uint32_t)ftr[jl], (uint32_t)ftr[jh]);
+      const uint64_t tr = isL ? Ltr : trf;
+      v[HF_FLAGS][k] = isL ? Lfl : fv(ffl);
+      v[HF_MASKS][k] = isL ? Lmk : fv(fmk);
+      v[HF_TERM][k] = isL ? Lterm : fv(fterm);
+      v[HF_COMMIT][k] = isL ? Lcommit : fv(fcommit);
+      v[HF_LEN][k] = isL ? Llen : fv(flen);
+      v[HF_DEADLINE][k] = isL ? Ldl : fv(fdl);
+      v[HF_QMETA][k] = isL ? pack_qmeta(0, 0, 0, __popc(rmask)) : pack_qmeta(0, fq, 0, 0);
+      v[HF_REQ_ARR][k] = isL ? INF : (fq ? fqa : INF);
+      v[HF_RES_ARR][k] = isL ? resA : INF;
+      v[HF_REQ_TAIL][k] = isL ? 0u : (fq ? fqa : 0u);
+      v[HF_RES_TAIL][k] = isL ? (rmask ? resA : 0u) : 0u;
+      v[HF_TRACE_LO][k] = (uint32_t)tr;
+      v[HF_TRACE_HI][k] = (uint32_t)(tr >> 32);
+    }
+    auto live = [](int q) {
+      return q < (int)(HF_ABASE * N) || (q >= (int)(HF_TRACE_LO * N) && q < (int)(HF_NEXT * N));
+    };
+    auto val = [&](int q) { return v[q / N][q % N]; };
+#if RS_LANE_STAGE
+    // into this lane's LDS row; the wave stores the rows' whole lines below
+#pragma unroll
+    for (int q = 0; q < (int)(HF_NEXT * N); ++q)
+      if (live(q)) myrow[q] = val(q);
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      const uint32_t qn = (HF_NEXT + fk(j)) * N + L, qm = (HF_NEXT + N + fk(j)) * N + L;
+      if (qn < (uint32_t)LW) myrow[qn] = (uint32_t)nx[j];
+      else blk[qn] = (uint32_t)nx[j];
+      if (qm < (uint32_t)LW) myrow[qm] = (uint32_t)mt[j];
+      else blk[qm] = (uint32_t)mt[j];
+    }
+#else
+#pragma unroll
+    for (int i = 0; i < (int)(HF_NEXT * N + 3) / 4; ++i) {
+      const int lo = 4 * i;
+      if (live(lo) && live(lo + 1) && live(lo + 2) && live(lo + 3)) {
+        reinterpret_cast<uint4*>(blk)[i] = make_uint4(val(lo), val(lo + 1), val(lo + 2), val(lo + 3));
+      } else {
+#pragma unroll
+        for (int q = lo; q < lo + 4; ++q)
+          if (live(q)) blk[q] = val(q);
+      }
+    }
+    // the leader's rows (node L): next / match of peer fk(j) + 1
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      blk[(HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
+      blk[(HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
+    }
+#endif
+    // queues back to the rings, heads at slot 0
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      if ((qmask >> j) & 1) {
+        uint4* dp = reinterpret_cast<uint4*>(qslots(S, c * N + fk(j), 0));
+        dp[0] = make_uint4(qA[j], RAFT_MSG_APPEND_ENTRIES | Lid << 3, qT[j], qa[j]);
+        dp[1] = make_uint4(qb[j], 0, 0, 0);
+      }
+    }
+    uint4* rp = reinterpret_cast<uint4*>(qslots(S, c * N + L, 1));
+    uint32_t n = 0;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      if ((rmask >> j) & 1) {
+        const uint32_t sid = fk(j) + 1;
+        uint4* dp = rp + 2 * n;
+        dp[0] = make_uint4(resA, RAFT_MSG_APPEND_RESPONSE | sid << 3 | rH[j] << 7, rT[j], rA[j]);
+        dp[1] = make_uint4(rB[j], 0, 0, 0);
+        ++n;
+      }
+    }
+  }
+#ifdef RS_WAVELOG
+  {
+    const uint64_t wl_end = wall_clock64();
+    const uint32_t emax = ~wave_min(~wl_events), emin = wave_min(wl_events);
+    if ((threadIdx.x & 63) == 0 && S.wavelog) {
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)(blockIdx.x * 4 + threadIdx.x / 64) * 32);
+      rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
+                          (uint32_t)(wl_end >> 32));
+      rec[1] = make_uint4(wl_trips, hw, xcc, wl_first);
+      rec[2] = make_uint4((uint32_t)(wl_loop - wl_start), (uint32_t)(wl_lend - wl_start), emin, emax);
+    }
+  }
+#endif
+#if RS_LANE_STAGE
+  __syncthreads();
+  {
+    // the written-back rows' whole lines (unchanged words were staged at the start)
+    const uint32_t cc = wb ? c : INF;
+#pragma unroll
+    for (int i = 0; i < LANE_CPW * U4 / 64; ++i) {
+      const uint32_t x = i * 64 + lane, b = x / U4, u = x - b * U4;
+      const uint32_t cb = (uint32_t)__shfl((int)cc, (int)b);
+      if (cb != INF) {
+        const uint32_t* r = tile + b * SW + 4 * u;
+        reinterpret_cast<uint4*>(S.hot + (size_t)cb * HB)[u] = make_uint4(r[0], r[1], r[2], r[3]);
+      }
+    }
+  }
+#endif
+  // counters: heartbeats, append-entries, append-responses; every message is delivered
+  if (nhb) atomicAdd(&sctr[0], nhb);
+  if (nae) atomicAdd(&sctr[1], nae);
+  if (nar) atomicAdd(&sctr[2], nar);
+  __syncthreads();
+  unsigned long long* const ctr = S.ctr + (size_t)(blockIdx.x % CTR_COPIES) * CTR_STRIDE;
+  if (threadIdx.x < 5) {
+    const uint32_t h = sctr[0], a = sctr[1], r = sctr[2];
+    const uint32_t msgs = (uint32_t)F * h + a;
+    const uint32_t x = threadIdx.x;
+    const int idx = x == 0 ? RAFT_CTR_EV_HEARTBEAT : x == 1 ? RAFT_CTR_EV_AE
+                  : x == 2 ? RAFT_CTR_EV_AR : x == 3 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
+    const uint32_t v = x == 0 ? h : x == 1 ? a : x == 2 ? r : msgs;
+    if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
+  }
+}
+
+
+// LDS beyond the 64 KiB default for the lane kernel's staging tiles (once, from configure_kernels)
+hipError_t configure_steady() {
+  hipError_t e = hipSuccess;
+#define RS_LANE_CFG(NN)                                                                      \
+  if (e == hipSuccess)                                                                       \
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(steady_lane_kernel<NN>),           \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lane_lds_bytes(NN));
+  RS_LANE_CFG(2) RS_LANE_CFG(3) RS_LANE_CFG(4) RS_LANE_CFG(5)
+#undef RS_LANE_CFG
+  return e;
+}
+
 // The steady kernel for N <= 5 (LITE launches; the caller checks). Grid: the packing's slots.
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0) {
   const uint32_t slots = S.perm ? sched_slots_bound(S.C, S.N) : S.C;
+  if (RS_STEADY_LANE) {
+    const dim3 grid((slots + LANE_CPB - 1) / LANE_CPB);
+    switch (S.N) {
+#define RS_LANE(NN)                                                                             \
+  case NN:                                                                                      \
+    hipExtLaunchKernelGGL((steady_lane_kernel<NN>), grid, dim3(LANE_WG), lane_lds_bytes(NN), st, \
+                          ev0, nullptr, 0, S, t0, nt);                                          \
+    break;
+      RS_LANE(2) RS_LANE(3) RS_LANE(4) RS_LANE(5)
+#undef RS_LANE
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (S.N) {
 #define RS_STEADY(NN)                                                                            \
   case NN:                                                                                       \

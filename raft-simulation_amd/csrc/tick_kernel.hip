@@ -1833,11 +1833,13 @@ hipError_t configure_n() {
   return hipSuccess;
 }
 
+hipError_t configure_steady();
+
 hipError_t configure_kernels() {
   hipError_t e = hipSuccess;
   if ((e = configure_n<2>()) || (e = configure_n<3>()) || (e = configure_n<4>()) ||
       (e = configure_n<5>()) || (e = configure_n<6>()) || (e = configure_n<7>()) ||
-      (e = configure_n<8>()) || (e = configure_n<9>()))
+      (e = configure_n<8>()) || (e = configure_n<9>()) || (e = configure_steady()))
     return e;
   return hipSuccess;
 }

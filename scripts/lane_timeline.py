@@ -1,0 +1,43 @@
+"""Per-wave timeline of the lane-per-cluster steady kernel from a -DRS_WAVELOG build (diagnostic
+only): wave start/end, load / loop / write-back split, loop trips and events per lane.
+Usage: lane_timeline.py LIB [clusters]"""
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "raft-simulation_amd")]
+from raftsim._backend import Backend  # noqa: E402
+
+C = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+sim = Backend(sys.argv[1], "raft_sim_", n_clusters=C, nodes=5, seed=42)
+for _ in range(6):
+    sim.step(10000)
+waves = 2 * C // 12 + 1000
+buf = (ctypes.c_uint32 * (waves * 32))()
+n = sim._lib.raftsim_diag_wavelog(sim._h, buf, waves)
+a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 32)[:n].astype(np.int64)
+a = a[(a[:, 0] | a[:, 1]) != 0]
+start = a[:, 0] | (a[:, 1] << 32)
+end = a[:, 2] | (a[:, 3] << 32)
+t0 = start.min()
+st, en = (start - t0) / 100.0, (end - t0) / 100.0
+q = lambda x: " ".join(f"{v:8.1f}" for v in np.percentile(x, [0, 10, 50, 90, 99, 100]))
+print(f"kernel_ms {sim.last_step_timing()[0]:.4f} waves {len(a)} span {en.max():.1f} us")
+print("start us    p0/10/50/90/99/100:", q(st))
+print("life us     p0/10/50/90/99/100:", q(en - st))
+print("load us     p0/10/50/90/99/100:", q(a[:, 8] / 100.0))
+print("loop us     p0/10/50/90/99/100:", q((a[:, 9] - a[:, 8]) / 100.0))
+print("wb us       p0/10/50/90/99/100:", q((end - start - a[:, 9]) / 100.0))
+print("trips       p0/10/50/90/99/100:", q(a[:, 4]))
+print("lanes on    p0/10/50/90/99/100:", q(a[:, 7]))
+print("events/lane min p0/10/50/90/99/100:", q(a[:, 10]))
+print("events/lane max p0/10/50/90/99/100:", q(a[:, 11]))
+print("us per trip p0/10/50/90/99/100:", q((a[:, 9] - a[:, 8]) / 100.0 / np.maximum(a[:, 4], 1)))
+hw, xcc = a[:, 5], a[:, 6]
+simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) & 7
+key = xcc * 10000 + se * 1000 + sh * 100 + cu * 4 + simd
+u, cnt = np.unique(key, return_counts=True)
+print("distinct SIMDs", len(u), "waves per SIMD p0/50/100", cnt.min(), np.median(cnt), cnt.max())
