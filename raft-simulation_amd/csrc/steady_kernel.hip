@@ -466,19 +466,14 @@ constexpr int LANE_WG = 256;
 #endif
 constexpr int LANE_CPW = RS_LANE_CPW;
 constexpr int LANE_CPB = LANE_WG / 64 * LANE_CPW;   // clusters per workgroup
-#ifndef RS_LANE_STAGE
-#define RS_LANE_STAGE 1
-#endif
-// words of each cluster block staged through LDS: fields FLAGS..TRACE_HI, whole lines
-__host__ __device__ constexpr int lane_stage_words(int N) { return (HF_NEXT * N + 31) / 32 * 32; }
-__host__ __device__ constexpr size_t lane_lds_bytes(int N) {
-  return RS_LANE_STAGE ? (size_t)(LANE_WG / 64) * LANE_CPW * (lane_stage_words(N) + 1) * 4 : 0;
-}
 #ifndef RS_STEADY_LANE
 #define RS_STEADY_LANE 1
 #endif
 #ifndef RS_LANE_DRAIN
 #define RS_LANE_DRAIN 1
+#endif
+#ifndef RS_LANE_ROUND
+#define RS_LANE_ROUND 1
 #endif
 
 // v = vals[k] for a runtime k < N, as masks (a select chain over an array is turned back into an
@@ -517,49 +512,27 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   uint32_t* const blk = S.hot + (size_t)c * HB;
 #ifdef RS_WAVELOG   // diagnostic build: per-wave timeline (scripts/lane_timeline.py)
   const uint64_t wl_start = wall_clock64();
-  uint32_t wl_trips = 0, wl_first = 0;
-  uint64_t wl_loop = 0;
+  uint32_t wl_trips = 0, wl_first = 0, wl_ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t wl_loop = 0, wl_ts = 0;
+#define RS_LPH(i)                                         \
+  do {                                                    \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();   \
+    wl_ph[i] += (uint32_t)(now_ - wl_ts);                 \
+    wl_ts = now_;                                         \
+  } while (0)
+#else
+#define RS_LPH(i) do {} while (0)
 #endif
 
-  // ------------------------------------------- load: fields FLAGS..RES_ARR, TRACE, checker hwm
+  // ------------------------------------------- load: fields FLAGS..RES_TAIL, TRACE, checker hwm
   uint32_t w[NW4 * 4];
 #pragma unroll
   for (int i = 0; i < NW4 * 4; ++i) w[i] = 0;
-#if RS_LANE_STAGE
-  // The first LW words of every block (fields FLAGS..TRACE_HI and the first rows) go through the
-  // wave's LDS tile: whole 128-B lines, eight per load instruction, instead of one 16-B piece of
-  // 64 different lines per instruction (a request per lane: the load and write-back phases were
-  // bound by L2 request rate, not bytes). Row stride LW + 1 (odd): lanes reading the same word of
-  // their own rows hit distinct banks.
-  constexpr int LW = lane_stage_words(N), SW = LW + 1, U4 = LW / 4;
-  extern __shared__ uint32_t lsm[];
-  uint32_t* const tile = lsm + (threadIdx.x / 64) * (LANE_CPW * SW);
-  uint32_t* const myrow = tile + (lane < (uint32_t)LANE_CPW ? lane : 0) * SW;
-  {
-    const uint32_t cc = active ? c : INF;
-#pragma unroll
-    for (int i = 0; i < LANE_CPW * U4 / 64; ++i) {
-      const uint32_t x = i * 64 + lane, b = x / U4, u = x - b * U4;
-      const uint32_t cb = (uint32_t)__shfl((int)cc, (int)b);
-      if (cb != INF) {
-        const uint4 v = reinterpret_cast<const uint4*>(S.hot + (size_t)cb * HB)[u];
-        uint32_t* r = tile + b * SW + 4 * u;
-        r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-      }
-    }
-  }
-  __syncthreads();
-  if (active) {
-#pragma unroll
-    for (int q = 0; q < (int)(HF_NEXT * N); ++q) w[q] = myrow[q];
-    w[CLW] = blk[CLW];
-  }
-#else
   if (active) {
 #pragma unroll
     for (int i = 0; i < NW4; ++i) {
       const int lo = 4 * i, hi = 4 * i + 3;
-      const bool need = lo < (int)(HF_REQ_TAIL * N) ||
+      const bool need = lo < (int)(HF_ABASE * N) ||
                         (hi >= (int)(HF_TRACE_LO * N) && lo < (int)(HF_NEXT * N)) ||
                         (lo <= (int)CLW && hi >= (int)CLW);
       if (need) {
@@ -568,7 +541,6 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       }
     }
   }
-#endif
   auto field = [&](int f, uint32_t (&out)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) out[k] = w[f * N + k];
@@ -630,14 +602,14 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   int32_t nx[F], mt[F];
 #pragma unroll
   for (int j = 0; j < F; ++j) {
-    const uint32_t qn = (HF_NEXT + fk(j)) * N + L, qm = (HF_NEXT + N + fk(j)) * N + L;
-#if RS_LANE_STAGE
-    nx[j] = active ? (int32_t)(qn < (uint32_t)LW ? myrow[qn] : blk[qn]) : 0;
-    mt[j] = active ? (int32_t)(qm < (uint32_t)LW ? myrow[qm] : blk[qm]) : 0;
-#else
-    nx[j] = active ? (int32_t)blk[qn] : 0;
-    mt[j] = active ? (int32_t)blk[qm] : 0;
-#endif
+    nx[j] = active ? (int32_t)blk[(HF_NEXT + fk(j)) * N + L] : 0;
+    mt[j] = active ? (int32_t)blk[(HF_NEXT + N + fk(j)) * N + L] : 0;
+  }
+  int32_t nx0[F], mt0[F];                     // as loaded: unchanged words are not stored back
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    nx0[j] = nx[j];
+    mt0[j] = mt[j];
   }
   const bool ackbad = Llen > w[CLW];          // a success response would be checker work (P4)
   const uint32_t Lkeys = Lmk >> 16;
@@ -714,6 +686,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   };
 #ifdef RS_WAVELOG
   wl_loop = wall_clock64();
+  wl_ts = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
     const uint32_t t = max(tn, next_event());
@@ -723,6 +696,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     if (!wl_trips) wl_first = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(on));
     ++wl_trips;
 #endif
+    RS_LPH(0);
     if (!on) continue;
     // ------------------------------------------------ decide on the pre-tick state
     const bool lres = rmask != 0 && resA <= t;               // a message beats the deadline
@@ -761,6 +735,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         if ((fae >> j) & 1)
           bail = bail || qb[j] != 0 || !(qT[j] < fterm[j] || flen[j] <= fcommit[j]);
     }
+    RS_LPH(1);
     if (bail) {                              // the general kernel runs this tick
       const uint32_t i = atomicAdd(S.nbail, 1u);
       S.bail_c[i] = c;
@@ -769,7 +744,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       continue;
     }
     // ------------------------------------------------ run
-    uint32_t tl = t;                         // the last tick run (the drain may run more)
+    uint32_t tl = t;                         // the last tick run (a round or a drain runs more)
+    bool round = false;
     if (lhb) {                               // heartbeat-handler: empty append-entries to all
 #pragma unroll
       for (int j = 0; j < F; ++j) {
@@ -780,30 +756,72 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       Ldl = t + S.hb;
       Ltr = trace_event(Ltr, t, 7, 0, 0, RAFT_LEADER, Lterm, 0);
       ++nhb;
+#if RS_LANE_ROUND
+      // The whole heartbeat round in this trip when nothing else can happen before its last
+      // response: every follower takes the append-entries at t + d (no follower deadline before
+      // it; the handler's checks pass), the followers' re-armed deadlines (>= t + d + el_base) and
+      // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the round
+      // ends before the launch does (and no older response is still queued). The responses then
+      // run as a drain (which stops at one outside the model; the next trip decides it).
+      round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > 2 * d + F;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
+#endif
     }
-    if (lres) {                              // append-response-handler, head in sender order
-      rmask &= rmask - 1;
-      if (!rmask) resA = INF;
-      Lmk |= xH << (16 + xid);
+    RS_LPH(2);
+    if (fae || round) {                      // append-entries-handler at each follower
+      // every follower's handler is computed and kept where it ran: the four Philox draws and
+      // trace hashes are independent chains the compiler interleaves (in a round every follower
+      // answers the same heartbeat on the same tick)
+      const uint32_t ta = round ? t + d : t;
+      const uint32_t fa = round ? (1u << F) - 1 : fae;
 #pragma unroll
       for (int j = 0; j < F; ++j) {
-        if (j == hs) {
-          nx[j] = xH ? (int32_t)xB : nx[j] - 1;
-          mt[j] = xH ? (int32_t)xA : mt[j];
+        const bool run_j = (fa >> j) & 1;
+        const uint32_t fid = fk(j) + 1;
+        const uint4 wd = event_draw(g, fid, ta, S);
+        const uint32_t mterm = qT[j], rterm = fterm[j];
+        const bool ok = mterm >= fterm[j];
+        const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER |
+                                       Lid << 6
+                                 : ffl[j];
+        const uint32_t nterm = ok ? mterm : fterm[j];
+        const uint64_t ntr = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3,
+                                         nterm, 0);
+        if (run_j) {
+          if (ok) {
+            fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
+            fmk[j] &= 0xFFFF0000u;
+          }
+          fterm[j] = nterm;
+          ffl[j] = nfl2;
+          // the response: to the leader's RES queue, in sender id order
+          rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
+          qA[j] = INF;
+          fdl[j] = ta + S.el_base + __umulhi(wd.y, S.el_span);
+          ftr[j] = ntr;
         }
       }
-      Ldl = t + S.hb;
-      Ltr = trace_event(Ltr, t, RAFT_MSG_APPEND_RESPONSE, xid, xT, RAFT_LEADER, Lterm, 0);
-      ++nar;
-#if RS_LANE_DRAIN
-      // the leader's next responses, one per tick, while nothing else in the cluster is due: the
-      // followers' next events (their deadlines; their queues are empty after they answered) and
-      // the launch end; the leader's own deadline moved past them. A response outside the model
-      // ends the drain and the next trip decides it.
+      qmask &= ~fa;
+      rmask = fa;
+      resA = ta + d;
+      nae += __popc(fa);
+      tl = ta;
+    }
+    RS_LPH(3);
+    if (lres || round) {                     // append-response-handler, heads in sender order
+      // from tick tau0 one response per tick while nothing else in the cluster is due (the
+      // followers' next events and the launch end; the leader's own deadline moves past each):
+      // the decided response at t, or a round's responses from t + 2d. A response outside the
+      // model ends the run of responses and the next trip decides it.
+      const uint32_t tau0 = round ? t + 2 * d : t;
       uint32_t E = tend;
 #pragma unroll
       for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
-      for (uint32_t tau = t + 1; rmask && tau < E; ++tau) {
+      if (lres) E = max(E, t + 1);           // decided: the first response runs
+      if (!RS_LANE_DRAIN) E = min(E, tau0 + 1);
+      for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
         const int h2 = __builtin_ctz(rmask);
         uint32_t yT = 0, yA = 0, yB = 0, yH = 0;
 #pragma unroll
@@ -829,44 +847,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         ++nar;
         tl = tau;
       }
-#endif
     }
-    if (fae) {                               // append-entries-handler at each follower
-      // every follower's handler is computed and kept where it ran: the four Philox draws and
-      // trace hashes are independent chains the compiler interleaves (in a round every follower
-      // answers the same heartbeat on the same tick)
-#pragma unroll
-      for (int j = 0; j < F; ++j) {
-        const bool run_j = (fae >> j) & 1;
-        const uint32_t fid = fk(j) + 1;
-        const uint4 wd = event_draw(g, fid, t, S);
-        const uint32_t mterm = qT[j], rterm = fterm[j];
-        const bool ok = mterm >= fterm[j];
-        const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER |
-                                       Lid << 6
-                                 : ffl[j];
-        const uint32_t nterm = ok ? mterm : fterm[j];
-        const uint64_t ntr = trace_event(ftr[j], t, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3,
-                                         nterm, 0);
-        if (run_j) {
-          if (ok) {
-            fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
-            fmk[j] &= 0xFFFF0000u;
-          }
-          fterm[j] = nterm;
-          ffl[j] = nfl2;
-          // the response: to the leader's RES queue, in sender id order
-          rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
-          qA[j] = INF;
-          fdl[j] = t + S.el_base + __umulhi(wd.y, S.el_span);
-          ftr[j] = ntr;
-        }
-      }
-      qmask &= ~fae;
-      rmask = fae;
-      resA = t + d;
-      nae += __popc(fae);
-    }
+    RS_LPH(4);
     tn = tl + 1;
   }
 
@@ -875,11 +857,19 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   const uint32_t wl_events = nhb + nae + nar;
 #endif
   // ---------------------------------------------------------------- write back
-  if (S.shist && wb && run) {
-    // packing key for the next launch (bailed clusters get theirs from the catch-up launch)
-    const uint32_t key = sched_bucket(next_event(), tend);
-    S.skey[c] = key;
-    atomicAdd(&S.shist[key], 1u);
+  if (S.shist) {
+    // packing key for the next launch (bailed clusters get theirs from the catch-up launch); the
+    // wave's clusters share a few keys: one histogram atomic per distinct key
+    const bool kl = wb && run;
+    const uint32_t key = kl ? sched_bucket(next_event(), tend) : INF;
+    if (kl) S.skey[c] = key;
+    uint64_t pend = __builtin_amdgcn_ballot_w64(kl);
+    while (pend) {
+      const uint32_t k = (uint32_t)__shfl((int)key, (int)__builtin_ctzll(pend));
+      const uint64_t same = __builtin_amdgcn_ballot_w64(kl && key == k);
+      if (lane == (uint32_t)__builtin_ctzll(pend)) atomicAdd(&S.shist[k], (uint32_t)__popcll(same));
+      pend &= ~same;
+    }
   }
   if (wb) {
     // every word of fields FLAGS..RES_TAIL and TRACE_LO/HI, from registers (LEN unchanged)
@@ -915,38 +905,30 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       return q < (int)(HF_ABASE * N) || (q >= (int)(HF_TRACE_LO * N) && q < (int)(HF_NEXT * N));
     };
     auto val = [&](int q) { return v[q / N][q % N]; };
-#if RS_LANE_STAGE
-    // into this lane's LDS row; the wave stores the rows' whole lines below
-#pragma unroll
-    for (int q = 0; q < (int)(HF_NEXT * N); ++q)
-      if (live(q)) myrow[q] = val(q);
-#pragma unroll
-    for (int j = 0; j < F; ++j) {
-      const uint32_t qn = (HF_NEXT + fk(j)) * N + L, qm = (HF_NEXT + N + fk(j)) * N + L;
-      if (qn < (uint32_t)LW) myrow[qn] = (uint32_t)nx[j];
-      else blk[qn] = (uint32_t)nx[j];
-      if (qm < (uint32_t)LW) myrow[qm] = (uint32_t)mt[j];
-      else blk[qm] = (uint32_t)mt[j];
-    }
-#else
+    // Only words that changed are stored (in a heartbeat round the deadlines and trace hashes do;
+    // flags, terms, masks, commits, queue words and rows come back unchanged): a lane's stores
+    // each go to a different cluster's block, one L2 request per lane, and the write-back of the
+    // whole grid at the launch end is bound by that request rate.
 #pragma unroll
     for (int i = 0; i < (int)(HF_NEXT * N + 3) / 4; ++i) {
       const int lo = 4 * i;
       if (live(lo) && live(lo + 1) && live(lo + 2) && live(lo + 3)) {
-        reinterpret_cast<uint4*>(blk)[i] = make_uint4(val(lo), val(lo + 1), val(lo + 2), val(lo + 3));
+        if (val(lo) != w[lo] || val(lo + 1) != w[lo + 1] || val(lo + 2) != w[lo + 2] ||
+            val(lo + 3) != w[lo + 3])
+          reinterpret_cast<uint4*>(blk)[i] =
+              make_uint4(val(lo), val(lo + 1), val(lo + 2), val(lo + 3));
       } else {
 #pragma unroll
         for (int q = lo; q < lo + 4; ++q)
-          if (live(q)) blk[q] = val(q);
+          if (live(q) && val(q) != w[q]) blk[q] = val(q);
       }
     }
     // the leader's rows (node L): next / match of peer fk(j) + 1
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      blk[(HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
-      blk[(HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
+      if (nx[j] != nx0[j]) blk[(HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
+      if (mt[j] != mt0[j]) blk[(HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
     }
-#endif
     // queues back to the rings, heads at slot 0
 #pragma unroll
     for (int j = 0; j < F; ++j) {
@@ -982,22 +964,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
                           (uint32_t)(wl_end >> 32));
       rec[1] = make_uint4(wl_trips, hw, xcc, wl_first);
       rec[2] = make_uint4((uint32_t)(wl_loop - wl_start), (uint32_t)(wl_lend - wl_start), emin, emax);
-    }
-  }
-#endif
-#if RS_LANE_STAGE
-  __syncthreads();
-  {
-    // the written-back rows' whole lines (unchanged words were staged at the start)
-    const uint32_t cc = wb ? c : INF;
-#pragma unroll
-    for (int i = 0; i < LANE_CPW * U4 / 64; ++i) {
-      const uint32_t x = i * 64 + lane, b = x / U4, u = x - b * U4;
-      const uint32_t cb = (uint32_t)__shfl((int)cc, (int)b);
-      if (cb != INF) {
-        const uint32_t* r = tile + b * SW + 4 * u;
-        reinterpret_cast<uint4*>(S.hot + (size_t)cb * HB)[u] = make_uint4(r[0], r[1], r[2], r[3]);
-      }
+      rec[3] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
+      rec[4] = make_uint4(wl_ph[4], 0, 0, 0);
     }
   }
 #endif
@@ -1019,17 +987,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 }
 
 
-// LDS beyond the 64 KiB default for the lane kernel's staging tiles (once, from configure_kernels)
-hipError_t configure_steady() {
-  hipError_t e = hipSuccess;
-#define RS_LANE_CFG(NN)                                                                      \
-  if (e == hipSuccess)                                                                       \
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(steady_lane_kernel<NN>),           \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lane_lds_bytes(NN));
-  RS_LANE_CFG(2) RS_LANE_CFG(3) RS_LANE_CFG(4) RS_LANE_CFG(5)
-#undef RS_LANE_CFG
-  return e;
-}
+hipError_t configure_steady() { return hipSuccess; }   // (no attributes needed)
 
 // The steady kernel for N <= 5 (LITE launches; the caller checks). Grid: the packing's slots.
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
@@ -1040,7 +998,7 @@ hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
     switch (S.N) {
 #define RS_LANE(NN)                                                                             \
   case NN:                                                                                      \
-    hipExtLaunchKernelGGL((steady_lane_kernel<NN>), grid, dim3(LANE_WG), lane_lds_bytes(NN), st, \
+    hipExtLaunchKernelGGL((steady_lane_kernel<NN>), grid, dim3(LANE_WG), 0, st, \
                           ev0, nullptr, 0, S, t0, nt);                                          \
     break;
       RS_LANE(2) RS_LANE(3) RS_LANE(4) RS_LANE(5)

@@ -28,6 +28,9 @@ for m in re.finditer(r'^(_ZN2rs\w+):\s', s, re.M):
     ms = re.match(r'rs::13steady_kernelILi(\d)E', pretty)
     if ms:
         pretty = f"steady_kernel<N={ms.group(1)}>"
+    ml = re.match(r'rs::18steady_lane_kernelILi(\d)E', pretty)
+    if ml:
+        pretty = f"steady_lane_kernel<N={ml.group(1)}>"
     print(f"{pretty[:48]:48s} {get('NumVgprs'):>5s} {get('TotalNumSgprs'):>5s} {get('ScratchSize'):>7s} {get('Occupancy'):>10s}")
 PY
 rm -f $S $S2

@@ -1,6 +1,6 @@
 """Per-wave timeline of the lane-per-cluster steady kernel from a -DRS_WAVELOG build (diagnostic
 only): wave start/end, load / loop / write-back split, loop trips and events per lane.
-Usage: lane_timeline.py LIB [clusters]"""
+Usage: lane_timeline.py LIB [clusters] [launches]"""
 import ctypes
 import sys
 from pathlib import Path
@@ -12,8 +12,9 @@ sys.path[:0] = [str(ROOT / "raft-simulation_amd")]
 from raftsim._backend import Backend  # noqa: E402
 
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+LAUNCHES = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 sim = Backend(sys.argv[1], "raft_sim_", n_clusters=C, nodes=5, seed=42)
-for _ in range(6):
+for _ in range(LAUNCHES):
     sim.step(10000)
 waves = 2 * C // 12 + 1000
 buf = (ctypes.c_uint32 * (waves * 32))()
@@ -41,3 +42,9 @@ simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) 
 key = xcc * 10000 + se * 1000 + sh * 100 + cu * 4 + simd
 u, cnt = np.unique(key, return_counts=True)
 print("distinct SIMDs", len(u), "waves per SIMD p0/50/100", cnt.min(), np.median(cnt), cnt.max())
+ph = a[:, 12:17].astype(np.float64)
+trips = np.maximum(a[:, 4], 1)[:, None]
+names = ("head", "decide", "heartbeat", "responses", "append-entries")
+print("shader cycles per trip (mean over waves): " + "  ".join(
+    f"{nm} {v:7.0f}" for nm, v in zip(names, (ph / trips).mean(axis=0))))
+print("shader cycles per wave (mean): " + "  ".join(f"{nm} {v:8.0f}" for nm, v in zip(names, ph.mean(axis=0))))

@@ -27,7 +27,13 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 KERNEL = "tick_kernel"
-STEADY = "steady_kernel"        # LITE launches: the steady kernel, then the catch-up tick kernel
+# LITE launches: the steady kernel (lane-per-cluster form, or the wave form), then the catch-up
+# tick kernel
+STEADY = ("steady_lane_kernel", "steady_kernel")
+
+
+def is_steady(name):
+    return any(s in name for s in STEADY)
 
 
 def launch_groups(rows, name_key):
@@ -36,10 +42,10 @@ def launch_groups(rows, name_key):
     groups = []
     for r in rows:
         nm = r[name_key]
-        if STEADY in nm:
+        if is_steady(nm):
             groups.append([r])
         elif KERNEL in nm:
-            if groups and len(groups[-1]) == 1 and STEADY in groups[-1][0][name_key]:
+            if groups and len(groups[-1]) == 1 and is_steady(groups[-1][0][name_key]):
                 groups[-1].append(r)
             else:
                 groups.append([r])
@@ -107,7 +113,7 @@ def main():
         # one value per counter per dispatch, then summed over each launch's dispatches
         disp = collections.OrderedDict()
         for r in rows:
-            if KERNEL in r["Kernel_Name"] or STEADY in r["Kernel_Name"]:
+            if KERNEL in r["Kernel_Name"] or is_steady(r["Kernel_Name"]):
                 e = disp.setdefault(r["Dispatch_Id"], {"Kernel_Name": r["Kernel_Name"], "c": {}})
                 e["c"][r["Counter_Name"]] = e["c"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         for g in launch_groups(list(disp.values()), "Kernel_Name"):
@@ -123,7 +129,7 @@ def main():
     groups = launch_groups(trace, "Kernel_Name")
     durs = [int(g[-1]["End_Timestamp"]) - int(g[0]["Start_Timestamp"]) for g in groups]
     stats = [r for r in csv.DictReader(open(src / "kt" / "run_kernel_stats.csv"))
-             if KERNEL in r["Name"] or STEADY in r["Name"]]
+             if KERNEL in r["Name"] or is_steady(r["Name"])]
     durs = durs[-max(1, bench["roofline"]["launches"]):]   # the timed launches, not the warm-up
     avg_ns = sum(durs) / max(1, len(durs))
 
