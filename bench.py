@@ -26,6 +26,9 @@ Per workload:
                 pmc_traffic.json (scripts/summarize_profile.py), used only when it was measured on
                 this kernel build (source hash) over this same window (steps, warm-up, window kind).
                 `bound` is the roofline axis (HBM); the measured limiter is named in `limiter`.
+                `frac_state_model` prices only the hot state in and out: a C2 launch on the
+                lane-per-cluster steady kernel keeps its messages in registers, so the event
+                model's 64 B per message is not HBM traffic there (PMC `traffic` shows it).
   cpu_baseline  the C oracle (oracle/raftref.c, the restatement of core.clj/log.clj; "port") on a
                 bounded sample of the same workload over the same tick window, clusters mapped over
                 every host CPU this process may run on (the pmap analogue), with the same
@@ -84,9 +87,11 @@ KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip", "raft-simulation_a
                   "raft-simulation_amd/csrc/raftsim.hip", "include/raftsim.h"]
 HALTS = ("halt_ioobe", "halt_npe", "halt_cce", "halt_overflow")
 LIMITER = {
-    "c2": "latency of each wave's chain of active trips (one wave's trips are serial; the launch "
-          "holds fewer waves than the chip has slots for two generations): PMC wave-cycle split "
-          "and per-wave timeline, DESIGN.md; not HBM bandwidth",
+    "c2": "one wave per SIMD running 64 clusters' heartbeat rounds: the chain of dependent "
+          "quarter-rate multiplies (Philox draws, FNV trace hash) per trip, then the state load "
+          "and the write-back's per-lane L2 requests (per-wave timeline, DESIGN.md); messages stay "
+          "in registers, so the event model's message bytes are not HBM traffic (see "
+          "frac_state_model and traffic)",
     "c3": "issue of the active trips' divergent instruction stream (client-set injections and "
           "redirect hops, most of them into halted nodes; PMC instruction counts, DESIGN.md), not "
           "HBM bandwidth",
@@ -275,7 +280,8 @@ def run_workload(name, args, world, rank, local_rank, dist):
     s_node = 32 + 8 * n
     msgs = delta["delivered"] / total_launches
     entries = delta["entries_appended"] / total_launches
-    event_bytes = 2 * s_node * count * n + 64 * msgs + 16 * entries
+    state_bytes = 2 * s_node * count * n
+    event_bytes = state_bytes + 64 * msgs + 16 * entries
     achieved = event_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms else 0.0
     ticks_per_launch = args.steps * TICKS_PER_STEP / max(1, launches)
     window = window_id(spec, args)
@@ -295,6 +301,11 @@ def run_workload(name, args, world, rank, local_rank, dist):
                      "model": "event: 2*S_node*nodes + 64 B/delivered msg + 16 B/appended entry "
                               "per launch",
                      "bytes_per_launch": event_bytes, "avg_launch_ms": avg_launch_ms,
+                     # the hot node state in and out once: what a launch that keeps its messages
+                     # on chip (the lane-per-cluster steady kernel) must move through HBM
+                     "state_bytes_per_launch": state_bytes,
+                     "frac_state_model": state_bytes / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                     if avg_launch_ms else 0.0,
                      "launches": launches, "ticks_per_launch": ticks_per_launch,
                      "kernel_src_sha": kernel_build_hash(),
                      "limiter": LIMITER["c2" if name == "c2" else "c3"]},

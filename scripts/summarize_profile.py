@@ -134,7 +134,10 @@ def main():
     avg_ns = sum(durs) / max(1, len(durs))
 
     n = bench["config"]["nodes"]
-    waves_ran = -(-bench["config"]["clusters_per_gpu"] // (64 // n))
+    # waves that simulate clusters: 64 // N clusters per wave on the general and wave-form steady
+    # kernels, 64 per wave on the lane-per-cluster steady kernel
+    lane_form = bool(groups) and any("steady_lane_kernel" in r["Kernel_Name"] for r in groups[-1])
+    waves_ran = -(-bench["config"]["clusters_per_gpu"] // (64 if lane_form else 64 // n))
     cal = calibration(src)
     (dst / f"{tag}_fetch_calibration.json").write_text(json.dumps(cal, indent=1) + "\n")
     roof = bench["roofline"]
@@ -175,7 +178,8 @@ def main():
             if avg.get("GRBM_GUI_ACTIVE") and "SQ_WAVE_CYCLES" in avg else None,
             # SQ_WAVES counts every launched wave, including the waves past the packing's slots
             # in use, which exit at once (the grid covers the padded packing's bound); per-wave
-            # figures divide by the waves that simulate clusters, ceil(clusters / (64 // N))
+            # figures divide by the waves that simulate clusters, ceil(clusters / (64 // N)), or
+            # ceil(clusters / 64) for the lane-per-cluster steady kernel
             "waves_launched": avg.get("SQ_WAVES"),
             "waves_with_clusters": waves_ran,
             "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / waves_ran
