@@ -73,6 +73,8 @@ struct DevSim {
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
   uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
                             // delay: the LITE tick kernel applies
+  uint32_t perm_dense;      // the packing was planned without padding (one slot per cluster:
+                            // nslots == C), for the lane-per-cluster steady kernel
   // Steady kernel hand-off (steady_kernel.hip): clusters it stops ("bails") at a tick it does not
   // model are listed here, and the catch-up launch of the general kernel (perm = bail_c, nslots =
   // nbail, resume = bail_t) runs them from that tick to the launch's end.

@@ -14,7 +14,7 @@ hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st
                        hipEvent_t ev1, bool steady);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
-                             hipStream_t st);
+                             hipStream_t st, bool dense);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -311,7 +311,11 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       };
       if (s->resort_ctr % every(s->resort_ctr) == 0) {
         if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream));
+        // LITE launches on the steady path: one slot per cluster, no padding (the lane kernel
+        // takes 64 consecutive slots per wave); otherwise chunks of whole waves
+        const bool dense = s->steady_ok && s->d.lite;
+        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream, dense));
+        s->d.perm_dense = dense;
         // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
         std::swap(s->d.shist, s->soff);
         s->d.perm = s->sperm;

@@ -994,7 +994,9 @@ hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
                          hipEvent_t ev0) {
   const uint32_t slots = S.perm ? sched_slots_bound(S.C, S.N) : S.C;
   if (RS_STEADY_LANE) {
-    const dim3 grid((slots + LANE_CPB - 1) / LANE_CPB);
+    // a dense packing has exactly one slot per cluster: no grid past the clusters
+    const uint32_t lslots = S.perm && !S.perm_dense ? slots : S.C;
+    const dim3 grid((lslots + LANE_CPB - 1) / LANE_CPB);
     switch (S.N) {
 #define RS_LANE(NN)                                                                             \
   case NN:                                                                                      \
