@@ -95,6 +95,10 @@ CASES = {
     # odd launch splits: queued messages cross launch boundaries into the pair cells
     "lite_odd_launches": dict(n_clusters=600, nodes=5, seed=81, ticks_per_launch=13, hb=60,
                               el_base=100, el_span=100, dmin=7, dmax=7),
+    # timers too short for the lane kernel's one-trip heartbeat round (hb < 2d + N - 1, el_base <
+    # d + N - 1): every round runs tick by tick, elections keep interrupting them
+    "lite_short_round": dict(n_clusters=1000, nodes=5, seed=85, hb=9, el_base=6, el_span=30,
+                             dmin=3, dmax=3),
 }
 
 
@@ -370,7 +374,7 @@ def test_gpu_steady_path_taken():
 
 
 LITE_CASES = ["c2_small", "lite_n2", "lite_n3", "lite_n4", "lite_elections", "lite_tiny_inbox",
-              "lite_odd_launches"]
+              "lite_odd_launches", "lite_short_round"]
 
 
 @pytest.mark.parametrize("name", LITE_CASES)
