@@ -95,6 +95,13 @@ def fnv(h, words):
     return h
 
 
+def fnv64(h, words):
+    """The trace hash's step (SIM_SPEC §4): the same multiply over 64-bit words."""
+    for w in words:
+        h = ((h ^ (w & M64)) * FNV_PRIME) & M64
+    return h
+
+
 # ----------------------------------------------------------------------------------------------
 # Halts (SIM_SPEC §4, D8): the Clojure exception that kills the node's loop
 # ----------------------------------------------------------------------------------------------
@@ -724,7 +731,7 @@ class PyCluster:
             except Halt as h:
                 self.fault[i] = h.code
                 self.cnt[["", "halt_ioobe", "halt_npe", "halt_cce", "halt_overflow"][h.code]] += 1
-                self.trace[i] = fnv(self.trace[i], self._trace_words(t, ev, msg, node, h.code))
+                self.trace[i] = fnv64(self.trace[i], self._trace_words(t, ev, msg, node, h.code))
                 continue
             self.nodes[i] = new
             self.cnt[COUNTERS[ev - 1]] += 1
@@ -747,7 +754,7 @@ class PyCluster:
                     self.deadline[i] = t + cfg["hb"]
             elif ev == 6 or stats["rearm"] or node["state"] == ":leader":
                 self.deadline[i] = election
-            self.trace[i] = fnv(self.trace[i], self._trace_words(t, ev, msg, new, 0))
+            self.trace[i] = fnv64(self.trace[i], self._trace_words(t, ev, msg, new, 0))
             for p, m in sends:
                 self.transmit(i, p, t, m, outbox, sides)
         # P2 delivery: receiver order, then sender id ascending, copy 0 then copy 1
@@ -762,7 +769,9 @@ class PyCluster:
     def _trace_words(self, t, ev, msg, node, fault):
         src = msg_src(msg) if msg is not None else 0
         mterm = msg.get("term", 0) if msg is not None else 0
-        return [t, ev, src, mterm, ROLE_CODE[node["state"]], node["current-term"], fault]
+        # two 64-bit words: (t, ev | src << 3 | role << 7 | fault << 9), (msg_term, current_term)
+        small = ev | src << 3 | ROLE_CODE[node["state"]] << 7 | fault << 9
+        return [t | small << 32, mterm | node["current-term"] << 32]
 
     def _violation(self, kind, t):
         self.cnt[kind] += 1

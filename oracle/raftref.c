@@ -391,9 +391,10 @@ static void redirect(tick_ctx_t* x, uint32_t k, const raft_msg_t* m, const uint3
 
 static uint64_t trace(uint64_t h, uint32_t t, uint32_t ev, uint32_t src, uint32_t mterm,
                       const raft_node_t* n, uint32_t fault) {
-  h = fnv(h, t); h = fnv(h, ev); h = fnv(h, src); h = fnv(h, mterm);
-  h = fnv(h, n->role); h = fnv(h, n->current_term); h = fnv(h, fault);
-  return h;
+  /* SIM_SPEC §4: two 64-bit words, (t | small << 32) then (msg_term | current_term << 32) */
+  const uint64_t small = ev | src << 3 | n->role << 7 | fault << 9;
+  h = (h ^ ((uint64_t)t | small << 32)) * FNV_PRIME;
+  return (h ^ ((uint64_t)mterm | (uint64_t)n->current_term << 32)) * FNV_PRIME;
 }
 
 static uint32_t popcount16(uint32_t v) { return (uint32_t)__builtin_popcount(v & 0xFFFF); }

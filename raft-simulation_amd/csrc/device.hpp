@@ -23,12 +23,6 @@
 
 namespace rs {
 
-// 1: each Philox round takes both halves of its two 32x32-bit products from one v_mad_u64_u32
-// each instead of a mul_lo + mul_hi pair (measured C4-N9 -5.5 %, C3 -1.6 %, C2 unchanged)
-#ifndef RS_PHILOX_MAD
-#define RS_PHILOX_MAD 1
-#endif
-
 constexpr uint32_t INF = 0xFFFFFFFFu;
 enum { P_INIT = 1, P_EVENT = 2, P_NET = 3, P_CLIENT = 4, P_PART = 6 };
 enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
@@ -75,16 +69,13 @@ struct DevSim {
                             // delay: the LITE tick kernel applies
   uint32_t perm_dense;      // the packing was planned without padding (one slot per cluster:
                             // nslots == C), for the lane-per-cluster steady kernel
-  // Steady kernel hand-off (steady_kernel.hip): clusters it stops ("bails") at a tick it does not
-  // model are listed here, and the catch-up launch of the general kernel (perm = bail_c, nslots =
-  // nbail, resume = bail_t) runs them from that tick to the launch's end.
-  uint32_t* bail_c;         // [C] bailed cluster ids
-  uint32_t* bail_t;         // [C] the tick each bailed cluster stopped before
+  // Steady kernel (steady_kernel.hip): clusters it stops ("bails") at a tick it does not model
+  // are run from that tick by the same workgroup through the general tick body; their count is
+  // summed here for the host's path choice (speed only).
   uint32_t* nbail;          // device word: clusters bailed this launch
-  uint32_t* nbail_zero;     // the next steady launch's word (two alternate), zeroed by this one
-  const uint32_t* resume;   // general kernel: per wave slot, the tick its cluster resumes at
-  uint32_t* bail_report;    // host-mapped word: the catch-up launch stores its cluster count there
-                            // (the host picks the next launches' path from it; speed only)
+  uint32_t* nbail_zero;     // the previous steady launch's word (two alternate): reported to
+                            // bail_report and zeroed by this launch
+  uint32_t* bail_report;    // host-mapped word (the host picks the next launches' path from it)
 };
 
 // Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
@@ -135,15 +126,11 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
                                         uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-#if RS_PHILOX_MAD
-    // one 32x32->64 product (v_mad_u64_u32) gives both halves
+    // one 32x32->64 product (v_mad_u64_u32) gives both halves (against a mul_lo + mul_hi pair:
+    // C4-N9 -5.5 %, C3 -1.6 %)
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-#else
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-#endif
     c0 = hi1 ^ c1 ^ k0;
     c1 = lo1;
     c2 = hi0 ^ c3 ^ k1;
@@ -206,16 +193,20 @@ __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;
 }
 
+// The trace hash's step (SIM_SPEC §4): FNV's multiply over two 64-bit words per event,
+// (t | (ev | src << 3 | role << 7 | fault << 9) << 32) then (msg_term | current_term << 32).
+// P = 2^40 + 0x1B3, so h * P = h * 0x1B3 + (h << 40): two products per word, both off the
+// other word's chain until the multiply.
+__device__ __forceinline__ uint64_t fnv64(uint64_t h, uint32_t lo, uint32_t hi) {
+  const uint32_t xl = (uint32_t)h ^ lo, xh = (uint32_t)(h >> 32) ^ hi;
+  // x * 0x1B3 + (x << 40): one v_mad_u64_u32 with the high word's products as its addend
+  return (uint64_t)xl * 0x1B3u + ((uint64_t)(xh * 0x1B3u + (xl << 8)) << 32);
+}
 __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t ev, uint32_t src,
                                                 uint32_t mterm, uint32_t role, uint32_t term,
                                                 uint32_t fault) {
-  h = fnv(h, t);
-  h = fnv(h, ev);
-  h = fnv(h, src);
-  h = fnv(h, mterm);
-  h = fnv(h, role);
-  h = fnv(h, term);
-  return fnv(h, fault);
+  h = fnv64(h, t, ev | src << 3 | role << 7 | fault << 9);
+  return fnv64(h, mterm, term);
 }
 
 // The EVENT draw of node id at tick t (SIM_SPEC §3): alts!! bit, timeout, rand-nth peer.

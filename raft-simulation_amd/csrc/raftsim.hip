@@ -54,17 +54,20 @@ struct Shard {
   uint32_t last_launches;
   unsigned long long* client_pw;
   // RAFT_SCHED_ALIGNED: the spare histogram (the schedule kernel zeroes it while reading d.shist;
-  // the two swap every launch) and the wave-slot -> cluster map of the next launch. keys_fresh:
-  // d.skey/d.shist hold a matching key set (from the previous tick launch). Only the first launch
-  // computes them from the state: after host writes the keys are merely stale, which changes the
-  // packing (speed), never the results.
+  // the two swap every rebuild) and the wave-slot -> cluster map of the next launch. keys_written:
+  // the last tick launch wrote every cluster's key and the matching histogram into d.skey /
+  // d.shist; otherwise a rebuild zeroes d.shist and computes both from the state (sched_key).
+  // Stale keys (after host writes or set_tick) change the packing (speed), never the results; a
+  // histogram always counts each cluster once, so a packing always places each cluster once.
   uint32_t *soff, *sperm, *snslots;   // + the slot count of the packing
-  bool keys_fresh;
-  uint64_t resort_ctr = 0;             // tick launches since create (RS_RESORT_EVERY)
+  bool keys_written;
+  uint64_t resort_ctr = 0;             // tick launches since create
+  uint32_t resort_every;               // rebuild period (fixed at create)
   // steady kernel (steady_kernel.hip): LITE launches at N <= 5 without TRACE; the two bail
-  // counters alternate between launches (each steady launch zeroes the other)
+  // counters alternate between steady launches (each reports and zeroes the other)
   bool steady_ok;
   bool last_steady;                    // the last tick launch took the steady path
+  bool steady_identity;                // steady launches run the clusters in id order (no packing)
   uint32_t* nbail2;
   uint32_t steady_parity;
   // Path choice per launch (speed only: both paths give the same state). RAFTSIM_STEADY=auto
@@ -77,24 +80,15 @@ struct Shard {
   uint32_t steady_cooldown;
 };
 constexpr uint32_t STEADY_COOLDOWN = 2;
-// 0: LITE launches always take the general kernel (A/B builds); results are the same either way
-#ifndef RS_STEADY
-#define RS_STEADY 1
-#endif
-// The wave packing is rebuilt every RS_RESORT_EVERY-th tick launch and reused in between: with
+// The wave packing is rebuilt every RESORT_EVERY-th tick launch and reused in between: with
 // key-pure waves a steady-state cluster keeps its wave mates' phase, so a packing stays good for
 // more than one 10k-tick launch, and skipping the schedule kernel (C2: 14.6 us) every other
 // launch measured C2 step wall 0.127 -> 0.119 ms with the tick kernel unchanged (every 4th: no
 // further gain). Results never depend on the packing.
-#ifndef RS_RESORT_EVERY
-#define RS_RESORT_EVERY 2
-#endif
-// LITE launches: a steady-state packing is a rotation of itself one launch later (every cluster's
-// next event moves by the same launch length), so after the first 8 launches (elections) it is
-// rebuilt less often
-#ifndef RS_RESORT_EVERY_LITE
-#define RS_RESORT_EVERY_LITE 8
-#endif
+constexpr uint32_t RESORT_EVERY = 2;
+// LITE handles: a steady-state packing is a rotation of itself one launch later (every cluster's
+// next event moves by the same launch length), so it is rebuilt every 8th launch
+constexpr uint32_t RESORT_EVERY_LITE = 8;
 
 // Exported functions take their C linkage from the declarations in include/raftsim.h.
 
@@ -225,21 +219,23 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   }
   d.client_pw = s->client_pw;
   d.wavelog = nullptr;
-#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
+#ifdef RS_WAVELOG
   if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {
     sh_destroy(s);
     return rc;
   }
 #endif
-  s->steady_ok = RS_STEADY && d.lite && s->N <= 5 && !d.TC && !(cfg->variant_flags & RAFT_VARIANT_SPEC);
-  if (s->steady_ok && ((rc = dalloc(s, &d.bail_c, s->C)) || (rc = dalloc(s, &d.bail_t, s->C)) ||
-                       (rc = dalloc(s, &s->nbail2, 2)))) {
+  s->steady_ok = d.lite && s->N <= 5 && !d.TC && !(cfg->variant_flags & RAFT_VARIANT_SPEC);
+  s->resort_every = d.lite ? RESORT_EVERY_LITE : RESORT_EVERY;
+  if (s->steady_ok && (rc = dalloc(s, &s->nbail2, 2))) {
     sh_destroy(s);
     return rc;
   }
   if (s->steady_ok) {
     const char* m = getenv("RAFTSIM_STEADY");
     s->steady_mode = m && !strcmp(m, "always") ? 1 : m && !strcmp(m, "never") ? 2 : 0;
+    const char* pk = getenv("RAFTSIM_STEADY_PACK");
+    s->steady_identity = pk && !strcmp(pk, "identity");
     s->steady_cooldown = 1;
     void* hp = nullptr;
     if (hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
@@ -300,44 +296,8 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
   for (uint32_t done = 0; done < n_ticks;) {
     const uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick;
-    uint32_t* keep_hist = nullptr;
-    if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
-      // pack clusters with the same next event onto the same waves for this launch: keys and
-      // histogram come from the previous tick launch, or are recomputed from the state. With
-      // RS_RESORT_EVERY = k > 1 the packing is rebuilt every k-th launch and reused in between
-      // (any packing gives the same results); only the launch before a rebuild writes keys.
-      auto every = [&](uint64_t ctr) -> uint64_t {
-        return s->d.lite && ctr >= 8 ? RS_RESORT_EVERY_LITE : RS_RESORT_EVERY;
-      };
-      if (s->resort_ctr % every(s->resort_ctr) == 0) {
-        if (!s->keys_fresh) HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
-        // LITE launches on the steady path: one slot per cluster, no padding (the lane kernel
-        // takes 64 consecutive slots per wave); otherwise chunks of whole waves
-        const bool dense = s->steady_ok && s->d.lite;
-        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream, dense));
-        s->d.perm_dense = dense;
-        // the schedule kernel read d.shist and zeroed soff: the next tick launch fills soff
-        std::swap(s->d.shist, s->soff);
-        s->d.perm = s->sperm;
-        s->d.nslots = s->snslots;
-        s->keys_fresh = true;
-      }
-      ++s->resort_ctr;
-      if (s->resort_ctr % every(s->resort_ctr) != 0) {   // no rebuild after this launch: no keys
-        keep_hist = s->d.shist;
-        s->d.shist = nullptr;
-      }
-    }
-    while (s->kev.size() < 2 * (size_t)(launches + 1)) {
-      hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
-      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
-      s->kev.push_back(e);
-    }
-#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
-    HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
-                          (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
-#endif
-    bool steady = s->steady_ok && s->d.lite;   // host writes may have cleared lite
+    // Path (speed only: both paths give the same state). Host writes may have cleared lite.
+    bool steady = s->steady_ok && s->d.lite;
     if (steady && s->steady_mode == 2) steady = false;
     if (steady && s->steady_mode == 0) {
       if (s->steady_cooldown) {
@@ -349,15 +309,58 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
         steady = false;
       }
     }
+    bool no_keys = false;                // this launch writes no packing keys
+    bool no_perm = false;
+    if (steady && s->steady_identity) {
+      // clusters in id order: no packing, no keys
+      no_perm = no_keys = true;
+      s->keys_written = false;
+    } else if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
+      // pack clusters with the same next event onto the same waves for this launch: keys and
+      // histogram come from the previous tick launch, or are computed from the state. The
+      // packing is rebuilt every resort_every-th launch and reused in between (any packing gives
+      // the same results); only the launch before a rebuild writes keys.
+      if (s->resort_ctr % s->resort_every == 0) {
+        if (!s->keys_written) {
+          HIP_OK(hipMemsetAsync(s->d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream));
+          HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
+        }
+        // LITE launches on the steady path: one slot per cluster, no padding (the lane kernel
+        // takes 64 consecutive slots per wave); otherwise chunks of whole waves. lite never comes
+        // back once cleared, so a packing used by a steady launch is always dense.
+        const bool dense = s->steady_ok && s->d.lite;
+        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream, dense));
+        s->d.perm_dense = dense;
+        // the schedule kernel read d.shist and zeroed soff: the next key-writing launch fills it
+        std::swap(s->d.shist, s->soff);
+        s->d.perm = s->sperm;
+        s->d.nslots = s->snslots;
+      }
+      ++s->resort_ctr;
+      s->keys_written = s->resort_ctr % s->resort_every == 0;   // the next launch rebuilds
+      no_keys = !s->keys_written;
+    }
+    if (steady && s->d.perm && !s->d.perm_dense) steady = false;   // (not reachable: see above)
+    while (s->kev.size() < 2 * (size_t)(launches + 1)) {
+      hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+      s->kev.push_back(e);
+    }
+#ifdef RS_WAVELOG
+    HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
+                          (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
+#endif
     s->last_steady = steady;
     if (steady) {
       s->d.nbail = s->nbail2 + s->steady_parity;
       s->d.nbail_zero = s->nbail2 + (s->steady_parity ^ 1);
       s->steady_parity ^= 1;
     }
-    HIP_OK(rs::launch_tick(s->d, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1],
+    DevSim D = s->d;
+    if (no_perm) D.perm = nullptr;
+    if (no_keys) D.shist = nullptr;
+    HIP_OK(rs::launch_tick(D, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1],
                            steady));
-    if (keep_hist) s->d.shist = keep_hist;
     done += nt;
     s->tick += nt;
     s->ticks_run += nt;
@@ -854,13 +857,9 @@ int raft_sim_set_tick(raft_sim_t* r, uint64_t tick) {
     const int rc = sh_sync(s);
     if (rc) return rc;
     s->tick = tick;
-    // the packing keys are relative to the next launch's first tick: recompute them, and drop
-    // the histogram the last tick launch filled (sched_key_kernel only adds to it)
-    if (s->keys_fresh && s->d.shist) {
-      HIP_OK(hipSetDevice(s->cfg.device));
-      HIP_OK(hipMemsetAsync(s->d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream));
-    }
-    s->keys_fresh = false;
+    // the packing keys are relative to the next launch's first tick: the next rebuild computes
+    // them from the state
+    s->keys_written = false;
   }
   r->tick = tick;
   return 0;
@@ -1006,7 +1005,7 @@ extern "C" int raftsim_diag_last_bails(raft_sim_t* r) {
 }
 
 
-#if defined(RS_WAVELOG) || defined(RS_REGIONCOUNT)
+#ifdef RS_WAVELOG
 // Diagnostic builds only (not part of include/raftsim.h): the per-wave timeline of shard 0's last
 // tick-kernel launch, 8 words per wave: start lo/hi, end lo/hi (100 MHz), active ticks, HW_ID,
 // XCC_ID, launch t0. Returns the number of waves.

@@ -1,480 +1,38 @@
-// steady_kernel.hip — the steady-state tick kernel of LITE launches for gfx950 (MI355X).
+// steady_kernel.hip — the steady-state kernel of LITE launches for gfx950 (MI355X).
 //
 // In a LITE launch (no client traffic, no faults, fixed delay: BASELINE config 2) a cluster that
 // has elected its leader repeats one heartbeat round forever: the leader's heartbeat broadcasts an
 // empty append-entries (heartbeat-handler, core.clj:162-164; append-entries-rpc 56-67), every
 // follower answers it (append-entries-handler 105-123) and the leader takes the answers, one per
 // tick (append-response-handler 141-149). This kernel runs exactly those events, bit for bit as
-// the general tick kernel does (SIM_SPEC.md §4), and nothing else: a cluster about to run any other
+// the general tick body does (SIM_SPEC.md §4), and nothing else: a cluster about to run any other
 // event (an election, a log entry, a halt, a message it cannot hold) is stopped ("bailed") before
-// that tick with its state written back, and the catch-up launch of the general kernel runs it from
-// that tick to the launch's end (DevSim::bail_c / bail_t / nbail). Results are therefore identical
-// to the general kernel's for any state; only the speed depends on how steady the clusters are.
+// that tick with its state written back, and the same workgroup then runs it from that tick to
+// the launch's end through the general tick body (tick_wave, CATCH form). Results are therefore
+// identical to the general kernel's for any state; only the speed depends on how steady the
+// clusters are. One dispatch per launch: there is no separate catch-up launch.
 //
-// What the narrow event set buys: no log arena, no HBM queue traffic and a small register set.
-// * Queues live in LDS for the whole launch. Every ordered (sender, receiver) pair of a cluster
-//   owns one 4-word cell (arrival, term, a, b | hdr << 24); a node's REQ and RES queues are lists of
-//   sender ids (4 bits each) in one VGPR. A message whose pair cell is still occupied, or one the
-//   cell cannot express (entries, a payload reference, b >= 2^24), bails its cluster. The HBM rings
-//   are read at launch start and written at the end (heads at slot 0; ring positions are not state).
-// * The leader-state rows (next-index / match-index) of the cluster's one ls_present node live in
-//   LDS; the other nodes' rows are never touched (a second ls_present node bails the cluster).
-// * Log length, arena cursors, last-led term and commit counts cannot change here, so they are
-//   neither loaded nor stored.
-// Registers: ~60 VGPRs against the general kernel's 117, so a wave slot per SIMD more than the
-// whole config-2 grid needs: one generation of waves instead of two.
+// Lane per cluster. One lane runs one whole cluster: the leader and its N-1 followers are named
+// registers (follower slot j is the j-th non-leader node in id order, so deliveries in sender
+// order are slot order), the messages in flight are registers too (a follower holds at most one
+// append-entries from the leader; the leader's append-responses all share one arrival and pop in
+// sender id order), and no event needs another lane: no shuffles, ballots or LDS inside the tick
+// loop. A wave runs 64 clusters; C2's 65,536 clusters are 1,024 waves, one per SIMD.
+//
+// What a heartbeat round costs is its multiplies: Philox draws (the followers' election timers)
+// and the trace hash. A follower's re-armed deadline (t + el_base + draw) is only compared with
+// ticks before the next append-entries reaches it, and in steady state (el_base > hb) none is, so
+// the draw is deferred: the deadline holds its lower bound t + el_base and a pending bit, and the
+// draw is made when a tick at or past that bound is about to be decided, or at write-back — one
+// draw per follower per launch instead of one per round, with identical results.
 #include <hip/hip_ext.h>
 
-#include "device.hpp"
+#include "tick_wave.hpp"
 
 namespace rs {
 
-constexpr int SCW = 4;   // words per pair cell: arrival, term, a, b | hdr << 24 (free: word 3 == 0)
-
-// clusters per wave (whole clusters, one lane per node)
-template <int N>
-constexpr int steady_cpw() { return 64 / N; }
-// words of pad after each cluster's cells (spreads the clusters' cells over the LDS banks)
-#ifndef RS_CPAD
-#define RS_CPAD 0
-#endif
-template <int N>
-constexpr int steady_cluster_words() { return N * (N - 1) * SCW + RS_CPAD; }
-template <int N>
-constexpr int steady_cell_words() { return steady_cpw<N>() * steady_cluster_words<N>(); }
-template <int N>
-constexpr size_t steady_lds_bytes() {
-  return (size_t)(steady_cell_words<N>() + steady_cpw<N>() * 2 * N + LCTR_WORDS) * sizeof(uint32_t);
-}
-
-// fl bits kept beside the packed flags word (pack_flags) while the kernel runs
-constexpr uint32_t SF_ACKBAD = 1u << 15;   // log_len > checker hwm: a success response is a check
-// every queued message of the REQ (RES) list has the head's arrival, so a pop knows the next head's
-// arrival without reading its cell (messages delivered in one tick share their arrival)
-constexpr uint32_t SF_REQSAME = 1u << 16, SF_RESSAME = 1u << 17;
-
-template <int N>
-__global__ void __launch_bounds__(64) steady_kernel(DevSim S, uint32_t t0, uint32_t nt) {
-  static_assert(N >= 2 && N <= 5, "4-bit sender lists of at most four entries");
-  constexpr int CPW = steady_cpw<N>();
-  constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
-  constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* const cells = smem;                      // [CPW][N][N-1][SCW] (+ pad per cluster)
-  int32_t* const rows = reinterpret_cast<int32_t*>(smem + steady_cell_words<N>());  // [CPW][2N]
-  uint32_t* const lctr = smem + steady_cell_words<N>() + CPW * 2 * N;
-  const int lane = threadIdx.x;
-  if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
-  if (blockIdx.x == 0 && lane == 0) *S.nbail_zero = 0;   // the bail counter of the next launch
-
-  const uint32_t wave = blockIdx.x;
-  const uint32_t nslots = S.perm ? *S.nslots : S.C;
-  if (wave * CPW >= nslots) return;
-  const int cs = lane / N, k = lane - cs * N;
-  const int bl = (cs < CPW ? cs : 0) * N;
-  const uint32_t slot = wave * CPW + cs;
-  const uint32_t c0 = cs < CPW && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
-  const bool active = c0 != INF;
-  const uint32_t c = active ? c0 : 0u;
-  const uint32_t g = S.goff + c, gi = c * N + k, id = k + 1;
-  const uint32_t peers = ALL & ~(1u << id);
-  const uint32_t cmask = (1u << N) - 1;
-  uint32_t* const hp = S.hot + (size_t)c * HB + k;
-  uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
-  int32_t* const myrows = rows + (cs < CPW ? cs : 0) * 2 * N;    // next[N], then match[N]
-  // this lane's pair cells: outgoing (to receiver index j) and incoming (from sender index s)
-  uint32_t* const ccells = cells + (cs < CPW ? cs : 0) * steady_cluster_words<N>();
-  auto cell_out = [&](int j) { return ccells + (k * (N - 1) + (j < k ? j : j - 1)) * SCW; };
-  auto cell_in = [&](int s) { return ccells + (s * (N - 1) + (k < s ? k : k - 1)) * SCW; };
-  if (cs < CPW) {                  // every pair cell starts free
-#pragma unroll
-    for (int j = 0; j < N - 1; ++j) ccells[(k * (N - 1) + j) * SCW + 3] = 0;
-  }
-  __builtin_amdgcn_wave_barrier();
-
-  auto cluster_any = [&](bool x) { return ((uint32_t)(__ballot(x) >> bl) & cmask) != 0; };
-  auto cluster_min = [&](uint32_t x) {
-    uint32_t m = x;
-#pragma unroll
-    for (int s = 0; s < N; ++s) m = min(m, (uint32_t)__shfl(x, bl + s));
-    return m;
-  };
-
-#ifdef RS_WAVELOG   // diagnostic build: per-wave timeline + per-phase cycles (scripts/wavelog_probe.py)
-  const uint64_t wl_start = wall_clock64();
-  uint32_t wl_trips = 0, wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t wl_ts = __builtin_amdgcn_s_memtime();
-#define RS_PHASE(i)                                          \
-  do {                                                       \
-    const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
-    wl_ph[i] += (uint32_t)(now_ - wl_ts);                    \
-    wl_ts = now_;                                            \
-  } while (0)
-#else
-#define RS_PHASE(i) do {} while (0)
-#endif
-  // ------------------------------------------------------------------ state load (launch start)
-  uint32_t fl = 0, mk = 0, term = 0, commit = 0, len = 0, deadline = INF, rqa = INF, rsa = INF;
-  uint32_t lists = 0;             // REQ senders (id) in nibbles 0-3, RES senders in nibbles 4-7
-  uint64_t trace = 0;
-  bool bad = false;               // the cluster's start state is outside this kernel's model
-  if (active) {
-    fl = hp[HF_FLAGS * N]; mk = hp[HF_MASKS * N];
-    term = hp[HF_TERM * N]; commit = hp[HF_COMMIT * N]; len = hp[HF_LEN * N];
-    deadline = hp[HF_DEADLINE * N];
-    const uint32_t qm = hp[HF_QMETA * N];
-    rqa = hp[HF_REQ_ARR * N]; rsa = hp[HF_RES_ARR * N];
-    trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
-    if (len > hc[0]) fl |= SF_ACKBAD;
-    // queued messages into the pair cells, in ring order
-    const uint32_t rqh = qm & 15, rqc = (qm >> 4) & 31, rsh = (qm >> 9) & 15, rsc = (qm >> 13) & 31;
-    if (rqc + rsc > N - 1) bad = true;
-    uint32_t used = 0;
-    for (uint32_t i = 0; i < rqc + rsc && !bad; ++i) {
-      const bool res = i >= rqc;
-      const uint32_t pos = wrapq((res ? rsh + i - rqc : rqh + i), S.Q);
-      const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, gi, res) + pos * qstride(S, res));
-      const uint4 m0 = mp[0], m1 = mp[1];
-      const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
-      if ((hdr >> 8) || m1.y || m1.z || m1.w || m1.x >= (1u << 24) || src < 1 || src > N ||
-          src == id || ((used >> src) & 1) || m0.x > t0 + S.dmin) {
-        bad = true;
-      } else {
-        used |= 1u << src;
-        *reinterpret_cast<uint4*>(cell_in(src - 1)) = make_uint4(m0.x, m0.z, m0.w, m1.x | hdr << 24);
-        const uint32_t n = res ? i - rqc : i;
-        lists |= src << (4 * n + (res ? 16 : 0));
-      }
-    }
-  }
-  // the leader-state rows of the cluster's ls_present node (at most one)
-  const bool lsp = active && ((fl >> 14) & 1);
-  const uint32_t lspm = (uint32_t)(__ballot(lsp) >> bl) & cmask;
-  bad = bad || __popc(lspm) > 1;
-  if (lsp) {
-#pragma unroll
-    for (int p = 0; p < 2 * N; ++p) myrows[p] = (int32_t)hp[(HF_NEXT + p) * N];
-  }
-  // a cluster outside the model from the start bails at t0 with its state untouched
-  const bool bad0 = cluster_any(bad);
-  if (active && bad0 && k == 0) {
-    const uint32_t i = atomicAdd(S.nbail, 1u);
-    S.bail_c[i] = c;
-    S.bail_t[i] = t0;
-  }
-  const bool wb = active && !bad0;          // state to write back at the end
-  bool run = wb;                            // the cluster still runs here (not bailed)
-  __builtin_amdgcn_wave_barrier();
-
-  RS_PHASE(9);
-  const uint32_t tend = t0 + nt, d = S.dmin;
-  uint32_t tnext = t0;
-  for (;;) {
-    const bool liv0 = run && !((fl >> 10) & 7);
-    uint32_t t = max(tnext, cluster_min(liv0 ? min(deadline, min(rqa, rsa)) : INF));
-    t = t < tend ? t : tend;
-    const bool on = run && t < tend;
-    if (!__ballot(on)) break;
-#ifdef RS_WAVELOG
-    ++wl_trips;
-#endif
-    RS_PHASE(8);
-    const bool live = on && !((fl >> 10) & 7);
-    const uint32_t role = fl & 3;
-    const bool rqok = live && rqa <= t, rsok = live && rsa <= t;
-    const bool ev = rqok || rsok || (live && t >= deadline);
-    // ------------------------------------------------ decide (no state changes yet)
-    // The EVENT draw: for the alts!! choice when both queues are ready, and for the next election
-    // timeout of a node that is not leader after the event (a follower's append-entries, a
-    // leader's append-entries of a newer term; core.clj:171-174).
-    uint4 w = make_uint4(0, 0, 0, 0);
-    if (ev && (rqok || role != RAFT_LEADER)) w = event_draw(g, id, t, S);
-    const int which = rqok && rsok ? (int)(w.x & 1) : rqok ? 0 : rsok ? 1 : -1;
-    const int s = which >= 0 ? (int)((lists >> (which ? 16 : 0)) & 15) - 1 : 0;
-    uint4 m = make_uint4(0, 0, 0, 0);
-    if (which >= 0) m = *reinterpret_cast<const uint4*>(cell_in(s));
-    const uint32_t mterm = m.y, ma = m.z, mb = m.w & 0xFFFFFFu, hdr = m.w >> 24;
-    const uint32_t type = hdr & 7, flag = (hdr >> 7) & 1, src = (uint32_t)s + 1;
-    const uint32_t keys = mk >> 16;
-    bool ok = true;
-    if (ev) {
-      if (which < 0) {
-        // heartbeat: leader with full leader-state, no LazySeq log, commit within the log (the
-        // IOOBE/NPE/CCE checks of append-entries-rpc pass), an empty broadcast (every peer's
-        // prev-index at or past the log's end) and every outgoing cell free. The row and cell
-        // reads are independent (all in flight at once).
-        ok = role == RAFT_LEADER && ((fl >> 14) & 1) && (keys & peers) == peers &&
-             !((fl >> 13) & 1) && commit <= len;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          if (j == k) continue;
-          const int32_t nx = myrows[j];
-          const uint32_t prev = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
-          ok = ok && prev >= len && prev < (1u << 24) && cell_out(j)[3] == 0;
-        }
-      } else if (which == 0) {
-        // append-entries with prev-index 0 and no entries (consistent without a log read); a
-        // newer term sets commit = log_len, which applies nothing when commit >= log_len
-        ok = type == RAFT_MSG_APPEND_ENTRIES && mb == 0 && (mterm < term || len <= commit) &&
-             cell_out(s)[3] == 0;
-      } else {
-        // append-response of no newer term to the row owner; a success response is checker
-        // work once the log passes the hwm (P4)
-        ok = type == RAFT_MSG_APPEND_RESPONSE && ((fl >> 14) & 1) && mterm <= term &&
-             (flag ? !(fl & SF_ACKBAD) : ((keys >> src) & 1) != 0);
-      }
-    }
-    if (cluster_any(ev && !ok)) {           // bail before this tick: the general kernel runs it
-      if (on && k == 0) {
-        const uint32_t i = atomicAdd(S.nbail, 1u);
-        S.bail_c[i] = c;
-        S.bail_t[i] = t;
-      }
-      run = false;
-      continue;
-    }
-    RS_PHASE(3);
-    // ------------------------------------------------ run the event
-    uint32_t sent = 0;             // receivers (bits 1..N); bit 31: replies (RES queues)
-    if (ev) {
-      uint32_t evc, tsrc = 0, tterm = 0;
-      if (which >= 0) {            // pop the head: free the cell, next head's arrival
-        cell_in(s)[3] = 0;
-        const int sh = which ? 16 : 0;
-        const uint32_t rest = ((lists >> sh) & 0xFFFFu) >> 4;
-        lists = (lists & ~(0xFFFFu << sh)) | rest << sh;
-        const uint32_t same = fl & (which ? SF_RESSAME : SF_REQSAME);
-        const uint32_t na = !rest ? INF : same ? (which ? rsa : rqa) : cell_in((int)(rest & 15) - 1)[0];
-        if (which) rsa = na;
-        else rqa = na;
-        tsrc = src;
-        tterm = mterm;
-      }
-      if (which < 0) {             // heartbeat-handler: append-entries to every peer
-        evc = 7;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          if (j == k) continue;
-          const int32_t nx = myrows[j];
-          const uint32_t pv = nx - 1 > 0 ? (uint32_t)(nx - 1) : 0u;
-          *reinterpret_cast<uint4*>(cell_out(j)) =
-              make_uint4(t + d, term, commit, pv | (RAFT_MSG_APPEND_ENTRIES | id << 3) << 24);
-        }
-        sent = peers;
-        lctr_add(lctr, RAFT_CTR_SENT, N - 1);
-      } else if (which == 0) {     // append-entries-handler
-        evc = RAFT_MSG_APPEND_ENTRIES;
-        uint32_t rh = RAFT_MSG_APPEND_RESPONSE | id << 3, ra = 0;
-        const uint32_t rterm = term;
-        if (mterm >= term) {
-          rh |= 1u << 7;
-          ra = ma;
-          commit = len;                                   // apply-entries! (nothing applied)
-          term = mterm;
-          // role :follwer, voted-for and votes cleared, leader-id = src, LazySeq flag cleared
-          fl = (fl & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER | src << 6;
-          mk &= 0xFFFF0000u;
-        }
-        *reinterpret_cast<uint4*>(cell_out(s)) = make_uint4(t + d, rterm, ra, rh << 24);
-        sent = 1u << src | 1u << 31;
-        lctr_add(lctr, RAFT_CTR_SENT, 1);
-      } else {                     // append-response-handler
-        evc = RAFT_MSG_APPEND_RESPONSE;
-        if (flag) {
-          mk |= 1u << (16 + src);
-          myrows[s] = (int32_t)mb;
-          myrows[N + s] = (int32_t)ma;
-        } else {
-          myrows[s] -= 1;
-        }
-      }
-      const uint32_t r2 = fl & 3;
-      deadline = r2 == RAFT_LEADER ? t + S.hb : t + S.el_base + __umulhi(w.y, S.el_span);
-      trace = trace_event(trace, t, evc, tsrc, tterm, r2, term, 0);
-      lctr_add(lctr, RAFT_CTR_EV_RV + evc - 1, 1);
-    }
-    RS_PHASE(4);
-    // ------------------------------------------------ P2: deliveries, in sender id order
-    if (__ballot(sent != 0)) {
-      uint32_t inm = 0, rep = 0;
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        const uint32_t sm = __shfl(sent, bl + j);
-        inm |= ((sm >> id) & 1u) << j;
-        rep |= (sm >> 31) << j;
-      }
-      if (!on) inm = 0;              // padding lanes alias cluster 0's lanes
-      while (inm) {
-        const int j = __builtin_ctz(inm);
-        inm &= inm - 1;
-        const int sh = ((rep >> j) & 1) ? 16 : 0;
-        const uint32_t q = (lists >> sh) & 0xFFFFu;
-        const uint32_t cnt = q ? (35u - __clz(q)) >> 2 : 0u;     // nibbles in use
-        if ((fl >> 10) & 7) {
-          lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
-          cell_in(j)[3] = 0;
-        } else if (cnt >= S.Q) {
-          lctr_add(lctr, RAFT_CTR_OVERFLOW, 1);
-          cell_in(j)[3] = 0;
-        } else {
-          lists |= (uint32_t)(j + 1) << (sh + 4 * cnt);
-          const uint32_t sb = sh ? SF_RESSAME : SF_REQSAME;
-          if (!cnt) {
-            fl |= sb;
-            if (sh) rsa = t + d;
-            else rqa = t + d;
-          } else if ((sh ? rsa : rqa) != t + d) {
-            fl &= ~sb;
-          }
-          lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-        }
-      }
-    }
-    RS_PHASE(5);
-    // ------------------------------------------------ the leader's append-response drain
-    // Ticks at which the cluster's only event is an append-response at its row owner (the leader)
-    // run here, one response per tick as above, without the cluster's trip: up to the cluster's
-    // next other event E (every other node's next event and the leader's REQ head), the leader's
-    // heartbeat tick, or a response outside the model (the trip then decides it).
-    const bool drl = on && lsp && (fl & (3u | 7u << 10)) == RAFT_LEADER && (lists >> 16) != 0;
-    if (__ballot(drl)) {
-      const uint32_t oth = !on || ((fl >> 10) & 7) ? INF : drl ? rqa : min(deadline, min(rqa, rsa));
-      const uint32_t E = min(cluster_min(oth), tend);
-      uint32_t tl = t;
-      if (drl) {
-        for (;;) {
-          const uint32_t tau = max(min(rsa, deadline), tl + 1);
-          if (tau >= E || rsa > tau) break;
-          const int hs = (int)((lists >> 16) & 15) - 1;
-          const uint4 x = *reinterpret_cast<const uint4*>(cell_in(hs));
-          const uint32_t xh = x.w >> 24, xf = (xh >> 7) & 1, xs = (uint32_t)hs + 1;
-          if ((xh & 7) != RAFT_MSG_APPEND_RESPONSE || x.y > term ||
-              (xf ? (fl & SF_ACKBAD) != 0 : ((mk >> (16 + xs)) & 1) == 0))
-            break;
-          cell_in(hs)[3] = 0;
-          const uint32_t rest = (lists >> 20) & 0xFFFu;
-          lists = (lists & 0xFFFFu) | rest << 16;
-          rsa = !rest ? INF : (fl & SF_RESSAME) ? rsa : cell_in((int)(rest & 15) - 1)[0];
-          if (xf) {
-            mk |= 1u << (16 + xs);
-            myrows[hs] = (int32_t)(x.w & 0xFFFFFFu);
-            myrows[N + hs] = (int32_t)x.z;
-          } else {
-            myrows[hs] -= 1;
-          }
-          deadline = tau + S.hb;
-          trace = trace_event(trace, tau, RAFT_MSG_APPEND_RESPONSE, xs, x.y, RAFT_LEADER, term, 0);
-          lctr_add(lctr, RAFT_CTR_EV_AR, 1);
-          tl = tau;
-        }
-      }
-      if (lspm) t = max(t, __shfl(tl, bl + __builtin_ctz(lspm)));   // the cluster takes its clock
-    }
-    RS_PHASE(6);
-    tnext = t + 1;
-  }
-#ifdef RS_WAVELOG
-  if (lane == 0 && S.wavelog) {
-    const uint64_t wl_end = wall_clock64();
-    uint32_t hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 32);
-    rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
-                        (uint32_t)(wl_end >> 32));
-    rec[1] = make_uint4(wl_trips, hw, xcc, 0);
-    rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
-    rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
-    rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
-    rec[5] = make_uint4(0, 0, 0, 0);
-  }
-#endif
-
-  // ------------------------------------------------------------------ write back
-  if (S.shist) {
-    // packing key for the next launch (as the general kernel's, keys of running clusters only:
-    // a bailed cluster's key comes from the catch-up launch)
-    const uint32_t me = wb && !((fl >> 10) & 7) ? min(deadline, min(rqa, rsa)) : INF;
-    const uint32_t cm = cluster_min(me);
-    const bool head = wb && run && k == 0;
-    const uint32_t key = head ? sched_bucket(cm, tend) : INF;
-    if (head) S.skey[c] = key;
-    const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
-    const uint32_t heads = (uint32_t)__popcll(__ballot(head));
-    if (kmin == kmax) {
-      if (lane == 0 && kmin != INF) atomicAdd(&S.shist[kmin], heads);
-    } else if (head) {
-      atomicAdd(&S.shist[key], 1u);
-    }
-  }
-  if (wb) {
-    hp[HF_FLAGS * N] = fl & 0x7FFFu;
-    hp[HF_MASKS * N] = mk;
-    hp[HF_TERM * N] = term; hp[HF_COMMIT * N] = commit; hp[HF_DEADLINE * N] = deadline;
-    hp[HF_TRACE_LO * N] = (uint32_t)trace; hp[HF_TRACE_HI * N] = (uint32_t)(trace >> 32);
-    // queues back to the rings, heads at slot 0; tail = the last message's arrival (0 if empty)
-    uint32_t cnt[2] = {0, 0}, tail[2] = {0, 0};
-#pragma unroll
-    for (int which = 0; which < 2; ++which) {
-      uint32_t q = (lists >> (which ? 16 : 0)) & 0xFFFFu;
-      uint32_t* qb = qslots(S, gi, which);
-      const size_t qs = qstride(S, which);
-      for (uint32_t i = 0; q; ++i, q >>= 4) {
-        const uint32_t sj = (q & 15) - 1;
-        const uint4 x = *reinterpret_cast<const uint4*>(cell_in((int)sj));
-        uint4* dp = reinterpret_cast<uint4*>(qb + i * qs);
-        dp[0] = make_uint4(x.x, x.w >> 24, x.y, x.z);
-        dp[1] = make_uint4(x.w & 0xFFFFFFu, 0, 0, 0);
-        cnt[which] = i + 1;
-        tail[which] = x.x;
-      }
-    }
-    hp[HF_QMETA * N] = pack_qmeta(0, cnt[0], 0, cnt[1]);
-    hp[HF_REQ_ARR * N] = rqa; hp[HF_RES_ARR * N] = rsa;
-    hp[HF_REQ_TAIL * N] = tail[0]; hp[HF_RES_TAIL * N] = tail[1];
-    if (lsp) {
-#pragma unroll
-      for (int p = 0; p < 2 * N; ++p) hp[(HF_NEXT + p) * N] = (uint32_t)myrows[p];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  unsigned long long* const ctr = S.ctr + (size_t)(wave % CTR_COPIES) * CTR_STRIDE;
-  if (lane < RAFT_CTR_COUNT) {
-    const uint32_t v = lctr[lane];
-    if (v) atomicAdd(&ctr[lane], (unsigned long long)v);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Lane-per-cluster form of the steady kernel. One lane runs one whole cluster: the leader and its
-// N-1 followers are named registers (follower slot j is the j-th non-leader node in id order), the
-// messages in flight are registers too (a follower holds at most one append-entries from the
-// leader; the leader's append-responses all share one arrival and pop in sender id order), and no
-// event needs another lane: no shuffles, ballots or LDS inside the tick loop, and a wave runs 64
-// clusters instead of 12. The events and their order are the steady kernel's (heartbeat-handler,
-// append-entries-handler and append-response-handler of core.clj:105-164, SIM_SPEC.md §4), and any
-// cluster outside this narrower model (no single leader with full leader-state, a halted node, a
-// message of another shape, a follower timing out, a response of a newer term, ...) is bailed
-// before that tick exactly as above, so results are the general kernel's for any state.
-// Grid: 256-thread workgroups, one cluster per thread, slots in the packing's order (clusters with
-// the same next event share a wave, so lanes take the same branch on every trip).
-constexpr int LANE_WG = 256;
-// clusters per wave: 64, or 32 (half the lanes idle, twice the waves: two per SIMD hide each
-// other's dependency latency)
-#ifndef RS_LANE_CPW
-#define RS_LANE_CPW 64
-#endif
-constexpr int LANE_CPW = RS_LANE_CPW;
-constexpr int LANE_CPB = LANE_WG / 64 * LANE_CPW;   // clusters per workgroup
-#ifndef RS_STEADY_LANE
-#define RS_STEADY_LANE 1
-#endif
-#ifndef RS_LANE_DRAIN
-#define RS_LANE_DRAIN 1
-#endif
-#ifndef RS_LANE_ROUND
-#define RS_LANE_ROUND 1
-#endif
+constexpr int LANE_WG = 256;                 // four waves, 64 clusters each
+constexpr int LANE_WAVES = LANE_WG / 64;
 
 // v = vals[k] for a runtime k < N, as masks (a select chain over an array is turned back into an
 // indexed load from memory by the compiler; this keeps the array in registers)
@@ -491,6 +49,12 @@ __device__ __forceinline__ uint32_t msel(bool a, uint32_t x, uint32_t y) {
   return (x & m) | (y & ~m);
 }
 
+// Dynamic LDS of a steady workgroup: one tick_wave LDS block per wave for the catch-up.
+template <int N>
+constexpr size_t steady_lds_bytes() {
+  return LANE_WAVES * block_lds_bytes<N, false>();
+}
+
 template <int N>
 __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   static_assert(N >= 2 && N <= 5, "follower masks and the response queue fit four followers");
@@ -498,14 +62,24 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
   constexpr int NW4 = (int)(CLW + 4) / 4;          // uint4s up to and including the checker hwm
   __shared__ uint32_t sctr[4];
+  __shared__ uint32_t nbl;                         // clusters this workgroup bailed
+  __shared__ uint32_t bl_c[LANE_WG], bl_t[LANE_WG];   // bailed cluster, tick it stopped before
+  extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
   const uint32_t nslots = S.perm ? *S.nslots : S.C;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *S.nbail_zero = 0;   // the next launch's bail counter
-  if (blockIdx.x * LANE_CPB >= nslots) return;                  // workgroup-uniform
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the previous steady launch's bail count (complete: that launch has ended) to the host, which
+    // picks the next launches' path from it (speed only); that word is this launch's successor's
+    const uint32_t prev = *S.nbail_zero;
+    if (S.bail_report) *S.bail_report = prev;
+    *S.nbail_zero = 0;
+  }
+  if (blockIdx.x * LANE_WG >= nslots) return;                  // workgroup-uniform
   if (threadIdx.x < 4) sctr[threadIdx.x] = 0;
+  if (threadIdx.x == 0) nbl = 0;
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t slot = blockIdx.x * LANE_CPB + threadIdx.x / 64 * LANE_CPW + lane;
-  const uint32_t c0 = lane < (uint32_t)LANE_CPW && slot < nslots ? (S.perm ? S.perm[slot] : slot)
-                                                                 : INF;
+  const uint32_t slot = blockIdx.x * LANE_WG + threadIdx.x;
+  const uint32_t c0 = slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
   const bool active = c0 != INF;
   const uint32_t c = active ? c0 : 0u;
   const uint32_t g = S.goff + c;
@@ -668,9 +242,9 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     if (!rmask) resA = INF;
   }
   if (active && bad) {                      // outside the model from the start: bail at t0
-    const uint32_t i = atomicAdd(S.nbail, 1u);
-    S.bail_c[i] = c;
-    S.bail_t[i] = t0;
+    const uint32_t i = atomicAdd(&nbl, 1u);
+    bl_c[i] = c;
+    bl_t[i] = t0;
   }
   const bool wb = active && !bad;
   bool run = wb;
@@ -678,6 +252,18 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   // ---------------------------------------------------------------- the cluster's ticks
   const uint32_t tend = t0 + nt, d = S.dmin;
   uint32_t tn = t0, nhb = 0, nae = 0, nar = 0;
+  // followers whose deadline holds its lower bound t_ae + el_base (the draw is deferred)
+  uint32_t fpend = 0;
+  auto draw_deadlines = [&](uint32_t due) {
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      if ((due >> j) & 1) {
+        const uint4 wd = event_draw(g, fk(j) + 1, fdl[j] - S.el_base, S);   // D4, core.clj:174
+        fdl[j] += __umulhi(wd.y, S.el_span);
+      }
+    }
+    fpend &= ~due;
+  };
   auto next_event = [&]() {
     uint32_t m = min(Ldl, resA);
 #pragma unroll
@@ -689,7 +275,17 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   wl_ts = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
-    const uint32_t t = max(tn, next_event());
+    uint32_t t = max(tn, next_event());
+    // a deferred deadline at or before the tick to decide is drawn first (it can only move later)
+    for (;;) {
+      uint32_t due = 0;
+#pragma unroll
+      for (int j = 0; j < F; ++j) due |= (uint32_t)(fdl[j] <= t) << j;
+      due &= fpend;
+      if (!run || t >= tend || !due) break;
+      draw_deadlines(due);
+      t = max(tn, next_event());
+    }
     const bool on = run && t < tend;
     if (!__builtin_amdgcn_ballot_w64(on)) break;
 #ifdef RS_WAVELOG
@@ -718,11 +314,11 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       }
     }
     const int hs = __builtin_ctz(rmask | (1u << F));
-    uint32_t xT = 0, xA = 0, xB = 0, xH = 0;
+    uint32_t xT = 0, xH = 0;
 #pragma unroll
     for (int j = 0; j < F; ++j) {
       if (j == hs) {
-        xT = rT[j]; xA = rA[j]; xB = rB[j]; xH = rH[j];
+        xT = rT[j]; xH = rH[j];
       }
     }
     const uint32_t xid = (uint32_t)hs + 1 + ((uint32_t)hs >= L ? 1u : 0u);
@@ -736,10 +332,10 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           bail = bail || qb[j] != 0 || !(qT[j] < fterm[j] || flen[j] <= fcommit[j]);
     }
     RS_LPH(1);
-    if (bail) {                              // the general kernel runs this tick
-      const uint32_t i = atomicAdd(S.nbail, 1u);
-      S.bail_c[i] = c;
-      S.bail_t[i] = t;
+    if (bail) {                              // the general tick body runs this tick
+      const uint32_t i = atomicAdd(&nbl, 1u);
+      bl_c[i] = c;
+      bl_t[i] = t;
       run = false;
       continue;
     }
@@ -756,31 +352,28 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       Ldl = t + S.hb;
       Ltr = trace_event(Ltr, t, 7, 0, 0, RAFT_LEADER, Lterm, 0);
       ++nhb;
-#if RS_LANE_ROUND
       // The whole heartbeat round in this trip when nothing else can happen before its last
       // response: every follower takes the append-entries at t + d (no follower deadline before
       // it; the handler's checks pass), the followers' re-armed deadlines (>= t + d + el_base) and
       // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the round
       // ends before the launch does (and no older response is still queued). The responses then
-      // run as a drain (which stops at one outside the model; the next trip decides it).
+      // run as a drain (which stops at one outside the model; the next trip decides it). A
+      // deferred deadline counts with its lower bound here (a round not taken is run tick by tick).
       round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > 2 * d + F;
 #pragma unroll
       for (int j = 0; j < F; ++j)
         round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
-#endif
     }
     RS_LPH(2);
     if (fae || round) {                      // append-entries-handler at each follower
-      // every follower's handler is computed and kept where it ran: the four Philox draws and
-      // trace hashes are independent chains the compiler interleaves (in a round every follower
-      // answers the same heartbeat on the same tick)
+      // every follower's handler is computed and kept where it ran: the trace hashes are
+      // independent chains the compiler interleaves (in a round every follower answers the same
+      // heartbeat on the same tick)
       const uint32_t ta = round ? t + d : t;
       const uint32_t fa = round ? (1u << F) - 1 : fae;
 #pragma unroll
       for (int j = 0; j < F; ++j) {
         const bool run_j = (fa >> j) & 1;
-        const uint32_t fid = fk(j) + 1;
-        const uint4 wd = event_draw(g, fid, ta, S);
         const uint32_t mterm = qT[j], rterm = fterm[j];
         const bool ok = mterm >= fterm[j];
         const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER |
@@ -799,10 +392,11 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           // the response: to the leader's RES queue, in sender id order
           rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
           qA[j] = INF;
-          fdl[j] = ta + S.el_base + __umulhi(wd.y, S.el_span);
+          fdl[j] = ta + S.el_base;                           // + the deferred draw
           ftr[j] = ntr;
         }
       }
+      fpend |= fa;
       qmask &= ~fa;
       rmask = fa;
       resA = ta + d;
@@ -820,7 +414,6 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #pragma unroll
       for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
       if (lres) E = max(E, t + 1);           // decided: the first response runs
-      if (!RS_LANE_DRAIN) E = min(E, tau0 + 1);
       for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
         const int h2 = __builtin_ctz(rmask);
         uint32_t yT = 0, yA = 0, yB = 0, yH = 0;
@@ -851,6 +444,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     RS_LPH(4);
     tn = tl + 1;
   }
+  draw_deadlines(fpend);                     // every deadline exact before it is stored
 
 #ifdef RS_WAVELOG
   const uint64_t wl_lend = wall_clock64();
@@ -858,7 +452,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #endif
   // ---------------------------------------------------------------- write back
   if (S.shist) {
-    // packing key for the next launch (bailed clusters get theirs from the catch-up launch); the
+    // packing key for the next launch (bailed clusters get theirs from the catch-up below); the
     // wave's clusters share a few keys: one histogram atomic per distinct key
     const bool kl = wb && run;
     const uint32_t key = kl ? sched_bucket(next_event(), tend) : INF;
@@ -973,6 +567,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   if (nhb) atomicAdd(&sctr[0], nhb);
   if (nae) atomicAdd(&sctr[1], nae);
   if (nar) atomicAdd(&sctr[2], nar);
+  // the bailed clusters' words are this workgroup's own stores: its waves see them after the
+  // barrier (same CU; no other workgroup reads them in this launch)
   __syncthreads();
   unsigned long long* const ctr = S.ctr + (size_t)(blockIdx.x % CTR_COPIES) * CTR_STRIDE;
   if (threadIdx.x < 5) {
@@ -984,40 +580,45 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     const uint32_t v = x == 0 ? h : x == 1 ? a : x == 2 ? r : msgs;
     if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
   }
+  // ---------------------------------------------------------------- catch-up
+  // The bailed clusters, each from the tick it stopped before to the launch's end, through the
+  // general tick body: wave w of the workgroup takes wave slots w, w + 4, ... of the list.
+  const uint32_t nb = nbl;
+  if (nb == 0) return;                                        // workgroup-uniform
+  if (threadIdx.x == 0) atomicAdd(S.nbail, nb);
+  const uint32_t wv = threadIdx.x >> 6;
+  tick_wave<N, false, false, true, true>(
+      S, t0, nt, dsm + wv * (block_lds_bytes<N, false>() / sizeof(uint32_t)), (int)lane, wv,
+      LANE_WAVES, bl_c, nb, bl_t, blockIdx.x * LANE_WAVES + wv);
 }
 
+hipError_t configure_steady() {
+  hipError_t e = hipSuccess;
+#define RS_CFG(NN)                                                                         \
+  if (e == hipSuccess)                                                                     \
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(steady_lane_kernel<NN>),         \
+                            hipFuncAttributeMaxDynamicSharedMemorySize,                    \
+                            (int)steady_lds_bytes<NN>());
+  RS_CFG(2) RS_CFG(3) RS_CFG(4) RS_CFG(5)
+#undef RS_CFG
+  return e;
+}
 
-hipError_t configure_steady() { return hipSuccess; }   // (no attributes needed)
-
-// The steady kernel for N <= 5 (LITE launches; the caller checks). Grid: the packing's slots.
+// The steady kernel for N <= 5 (LITE launches; the caller checks): one thread per packing slot,
+// which is one per cluster (dense packing or the identity). Its timestamps go into ev0/ev1 through
+// its dispatch packet.
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
-                         hipEvent_t ev0) {
-  const uint32_t slots = S.perm ? sched_slots_bound(S.C, S.N) : S.C;
-  if (RS_STEADY_LANE) {
-    // a dense packing has exactly one slot per cluster: no grid past the clusters
-    const uint32_t lslots = S.perm && !S.perm_dense ? slots : S.C;
-    const dim3 grid((lslots + LANE_CPB - 1) / LANE_CPB);
-    switch (S.N) {
+                         hipEvent_t ev0, hipEvent_t ev1) {
+  if (S.perm && !S.perm_dense) return hipErrorInvalidValue;   // padded slots: not this kernel's
+  const dim3 grid((S.C + LANE_WG - 1) / LANE_WG);
+  switch (S.N) {
 #define RS_LANE(NN)                                                                             \
   case NN:                                                                                      \
-    hipExtLaunchKernelGGL((steady_lane_kernel<NN>), grid, dim3(LANE_WG), 0, st, \
-                          ev0, nullptr, 0, S, t0, nt);                                          \
+    hipExtLaunchKernelGGL((steady_lane_kernel<NN>), grid, dim3(LANE_WG), steady_lds_bytes<NN>(), \
+                          st, ev0, ev1, 0, S, t0, nt);                                          \
     break;
-      RS_LANE(2) RS_LANE(3) RS_LANE(4) RS_LANE(5)
+    RS_LANE(2) RS_LANE(3) RS_LANE(4) RS_LANE(5)
 #undef RS_LANE
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  switch (S.N) {
-#define RS_STEADY(NN)                                                                            \
-  case NN:                                                                                       \
-    hipExtLaunchKernelGGL((steady_kernel<NN>),                                                   \
-                          dim3((slots + steady_cpw<NN>() - 1) / steady_cpw<NN>()), dim3(64),     \
-                          steady_lds_bytes<NN>(), st, ev0, nullptr, 0, S, t0, nt);              \
-    break;
-    RS_STEADY(2) RS_STEADY(3) RS_STEADY(4) RS_STEADY(5)
-#undef RS_STEADY
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

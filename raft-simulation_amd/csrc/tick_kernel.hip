@@ -1,1457 +1,20 @@
-// tick_kernel.hip — the batched Raft tick kernel for gfx950 (MI355X) and its helpers.
-//
-// One lane per node, one wave per floor(64/N) clusters, `nt` ticks fused per launch with all hot
-// node state in VGPRs. Per tick a lane does the reference's `wait` (src/raft/core.clj:176-195) once:
-// pick at most one event (D3), run the handler (core.clj:91-169, log.clj:5-87), emit messages into
-// LDS cells, then — only when some lane of the wave did something — the wave runs the network
-// (P2), log transfer (P3) and checker (P4) phases of SIM_SPEC.md §4. Idle ticks cost a handful of
-// VALU instructions and one ballot.
+// tick_kernel.hip — the general tick kernel for gfx950 (MI355X) and its helpers: the wave packing
+// (schedule kernels), init-node, the per-cluster digest and the launchers. The tick body itself is
+// tick_wave (tick_wave.hpp).
 #include <hip/hip_ext.h>
 
-#include "device.hpp"
+#include "tick_wave.hpp"
 
 namespace rs {
 
-__device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) {
-  atomicAdd(&lctr[kind], 1u);
-  atomicMin(&lctr[LCTR_FIRSTVIOL], t);
-}
-
-// LDS message cells. A node emits either one broadcast or one reply per tick, and the words
-// (term, a) of a broadcast are the same for every peer, so they live once per sender in a 2-word
-// sender record; each (sender, receiver) pair cell holds the other six: hdr, b, eterm, eval, poff
-// and the delivery pack transmit() adds. 26 words per five-node sender instead of 32 keeps a
-// block of four waves under 1/6 of the CU's LDS.
-constexpr int CELLW = 6;
-constexpr int SRECW = 2;
-
-// One emitted message a = (hdr, term, a, b), b = (eterm, eval, poff, -) into its pair cell (the
-// sender record is written once per emission by the caller).
-__device__ __forceinline__ void cell_put(uint32_t* cl, uint4 a, uint4 b) {
-  reinterpret_cast<uint2*>(cl)[0] = make_uint2(a.x, a.w);
-  reinterpret_cast<uint2*>(cl)[1] = make_uint2(b.x, b.y);
-  cl[4] = b.z;
-}
-
-// P2 fault draws for one emitted message whose words are already in cell `cl`: the delivery pack
-// (copy delays and count) goes to the cell's last word and the receiver's bit into sentmask.
-template <int N, bool LITE>
-__device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
-                                         uint32_t p, bool part, uint32_t sides, uint32_t* cl,
-                                         uint32_t& sentmask, uint32_t* lctr) {
-  // RAFT_CTR_SENT is counted by the caller (once per emission: 1 or N - 1)
-  if (part && (((sides >> id) ^ (sides >> p)) & 1)) {
-    lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
-    return;
-  }
-  uint32_t pack;
-  if (LITE || (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax)) {
-    pack = S.dmin | 1u << 16;
-  } else {
-    const uint4 w = philox(g, id | P_NET << 8, t, p, S.key0, S.key1);
-    if (ppm(w.x) < S.drop_ppm) {
-      lctr_add(lctr, RAFT_CTR_DROPPED, 1);
-      return;
-    }
-    const uint32_t span = S.dmax - S.dmin + 1;
-    pack = (S.dmin + __umulhi(w.z, span)) | 1u << 16;
-    if (ppm(w.y) < S.dup_ppm) {
-      lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
-      pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
-    }
-  }
-  cl[CELLW - 1] = pack;
-  sentmask |= 1u << p;
-}
-
-// A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are fields
-// of the cluster block (stride N); kernels with a small N keep the wave's rows in LDS for the whole
-// launch (NM_LDS below) so heartbeats and append-responses pay no global round trip for them.
-struct PeerW {
-  int32_t* nx;
-  int32_t* mt;
-  uint32_t stride;
-  __device__ __forceinline__ int32_t& next(uint32_t p) const { return nx[p * stride]; }
-  __device__ __forceinline__ int32_t& match(uint32_t p) const { return mt[p * stride]; }
-};
-
-// F3: record one `wait` iteration (core.clj:182-186) — the node map before the handler and the
-// message alts!! returned — as a raft_trace_event_t (32 words) in the node's ring.
-template <int N>
-__device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint32_t t,
-                                             const NodeR& n, const PeerW& lsw, uint4 m0, uint4 m1,
-                                             uint32_t tes) {
-  const uint32_t seq = S.tcount[gi];
-  S.tcount[gi] = seq + 1;
-  uint32_t w[32];
-  w[0] = t; w[1] = seq;
-  w[2] = m0.x; w[3] = m0.y; w[4] = m0.z; w[5] = m0.w;
-  w[6] = m1.x; w[7] = m1.y; w[8] = m1.z; w[9] = m1.w;
-  w[10] = n.role | n.vf << 8 | n.lid << 16 | n.lsp << 24;
-  w[11] = n.votes | n.keys << 16;
-  w[12] = n.term;
-#pragma unroll
-  for (int p = 0; p < RAFT_MAX_NODES; ++p) {
-    w[13 + p] = p < N ? (uint32_t)lsw.next(p) : 0u;
-    w[22 + p] = p < N ? (uint32_t)lsw.match(p) : 0u;
-  }
-  w[31] = tes;
-  uint4* rec = reinterpret_cast<uint4*>(S.tr + ((size_t)gi * S.TC + seq % S.TC) * 32);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-}
-
-// Log Matching over cnt consecutive positions of two logs whose first slots are xi in arena xa
-// and yi in arena ya (slots wrap at A): is there a position with the same term and a different
-// value? Four positions per trip with their eight loads in flight together (a 2000-entry
-// AppendEntries is checked against every peer: one memory round trip per entry was most of C4's
-// time); every slot read is inside the arena, the comparisons past cnt are masked.
-template <int W = 4>
-__device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
-                                             uint32_t yi, uint32_t cnt, uint32_t A) {
-  for (uint32_t i = 0; i < cnt; i += W) {
-    uint2 x[W], y[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      x[j] = xa[xi];
-      y[j] = ya[yi];
-      xi = xi + 1 == A ? 0 : xi + 1;
-      yi = yi + 1 == A ? 0 : yi + 1;
-    }
-    bool c = false;
-#pragma unroll
-    for (int j = 0; j < W; ++j) c |= i + j < cnt && x[j].x == y[j].x && x[j].y != y[j].y;
-    if (c) return true;
-  }
-  return false;
-}
-
-// Copy `cnt` arena entries from slot si of `src` to slot di of `dst` (slots wrap at A), eight per
-// batch: a batch's loads are all issued before its stores, so a long copy pays one memory round
-// trip per eight entries rather than one per entry. Ascending order with every load of a batch
-// ahead of its stores keeps an overlapping relocation (dst ahead of src by d < A) exact: a slot
-// is only overwritten after it has been read, as in the oracle's element-by-element copy.
-#ifndef RS_COPY_BATCH
-#define RS_COPY_BATCH 4
-#endif
-template <uint32_t B = RS_COPY_BATCH>
-__device__ __forceinline__ void arena_copy(uint2* dst, uint32_t di, const uint2* src, uint32_t si,
-                                           uint32_t cnt, uint32_t A) {
-  uint32_t i = 0;
-  if (A >= B) {
-    for (; i + B <= cnt; i += B) {
-      uint2 v[B];
-#pragma unroll
-      for (int j = 0; j < (int)B; ++j) {
-        const uint32_t s = si + j;
-        v[j] = src[s >= A ? s - A : s];
-      }
-#pragma unroll
-      for (int j = 0; j < (int)B; ++j) {
-        const uint32_t d = di + j;
-        dst[d >= A ? d - A : d] = v[j];
-      }
-      si += B;
-      si = si >= A ? si - A : si;
-      di += B;
-      di = di >= A ? di - A : di;
-    }
-  }
-  for (; i < cnt; ++i) {
-    dst[di] = src[si];
-    si = si + 1 == A ? 0 : si + 1;
-    di = di + 1 == A ? 0 : di + 1;
-  }
-}
-
-// F4 Spec-Raft control (SIM_SPEC §8): one event of a running node under Raft's Figure 2 rules.
-// NOT reference behaviour. Same contract as the faithful handler below it in tick_kernel: decide
-// `fault` (OVERFLOW only) before touching the node, then mutate `n` in place and describe the
-// emission (emit/ra/rb), the leader-state writes (nm) and the P3 log plan.
-template <int N, uint32_t MAJ>
-__device__ __forceinline__ void spec_handle(
-    const DevSim& S, NodeR& n, const PeerW& lsw, const uint2* sar, const uint32_t* fr,
-    uint32_t* lctr, int which,
-    uint32_t id, int k, int bl, uint32_t sgi, uint32_t peers, uint4 m0, uint4 m1,
-    uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
-    uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
-    uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg,
-    bool& rearm) {
-  const uint32_t A = S.A;
-  if (which < 0) {
-    if (n.role == RAFT_LEADER) {                                  // heartbeat
-      ev = 7;
-      emit = 2;
-    } else {                                                      // election timeout
-      ev = 6;
-      uint32_t ep = 0, et = 0, evl = 0;
-      if (n.len) {
-        const uint2 e = sar[(n.base + n.len - 1) % A];
-        ep = 1; et = e.x; evl = e.y;
-      }
-      n.role = RAFT_CANDIDATE; n.vf = id; n.votes = 1u << id; n.term += 1;
-      ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, n.term, n.len, 0);
-      rb = make_uint4(et, evl, 0, 0);
-      emit = 1;
-    }
-    return;
-  }
-  const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mpoff = m1.w;
-  const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
-                 mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
-  ev = type;
-  // OVERFLOW, the only Spec-Raft halt, is decided on the pre-event state
-  bool consistent = false;
-  if (type == RAFT_MSG_APPEND_ENTRIES && mterm >= n.term) {
-    consistent = mb == 0;
-    if (!consistent && mb <= n.len && mep) consistent = sar[(n.base + mb - 1) % A].x == met;
-    if (consistent && mb + pcnt > S.L) fault = RAFT_FAULT_OVERFLOW;
-  }
-  if (type == RAFT_MSG_CLIENT_SET && n.role == RAFT_LEADER && n.len + 1 > S.L)
-    fault = RAFT_FAULT_OVERFLOW;
-  if (fault) return;
-  if (type != RAFT_MSG_CLIENT_SET && mterm > n.term) {          // term rule: step down
-    n.term = mterm; n.vf = 0; n.votes = 0; n.lid = 0; n.role = RAFT_FOLLOWER;
-    if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
-  }
-  switch (type) {
-    case RAFT_MSG_REQUEST_VOTE: {
-      const uint32_t lt = n.len ? sar[(n.base + n.len - 1) % A].x : 0u;
-      const uint32_t mt = mep ? met : 0u;
-      const bool up = (S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) || mt > lt ||
-                      (mt == lt && ma >= n.len);
-      const uint32_t grant = mterm == n.term && (n.vf == 0 || n.vf == src) && up;
-      ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
-      if (grant) {
-        n.vf = src;
-        rearm = true;                       // Figure 2: granting a vote resets the timer
-      }
-      emit = 3;
-      break;
-    }
-    case RAFT_MSG_APPEND_ENTRIES: {
-      ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
-      emit = 3;
-      if (mterm < n.term) break;
-      n.role = RAFT_FOLLOWER; n.votes = 0; n.lid = src;
-      rearm = true;                         // AppendEntries from the current leader
-      if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
-      if (!consistent) break;
-      // first conflict in [b, min(len, b + pcnt)); the payload is read from the sender's arena,
-      // an entry its pre-tick frontier has overwritten reading (0, 0)
-      const uint64_t sf0 = fr[bl + (int)src - 1];
-      const uint2* sa = arena_of(S, sgi - k + src - 1);
-      const uint32_t hi = n.len < mb + pcnt ? n.len : mb + pcnt;
-      uint32_t kk = mb, evc = 0;
-      for (; kk < hi; ++kk) {
-        const uint32_t i = kk - mb;
-        uint32_t pt = 0;
-        if (sf0 > (uint64_t)mpoff + i + A) ++evc;
-        else pt = sa[(mpoff + i) % A].x;
-        if (sar[(n.base + kk) % A].x != pt) break;
-      }
-      lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evc);
-      const uint32_t mc = mb + pcnt - kk;
-      if (mc) {                               // truncate at kk, append payload [kk - b, pcnt)
-        pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff + (kk - mb); ppcnt = mc;
-        pold_base = n.base;
-        if (kk < n.len || n.base + n.len != n.front) {
-          preloc = 1;
-          n.base = n.front;
-          n.front += kk;
-        }
-        n.front += mc;
-        n.len = mb + pcnt;
-        appended = mc;
-      }
-      if (ma > n.commit) {
-        const uint32_t nc = ma < mb + pcnt ? ma : mb + pcnt;
-        if (nc > n.commit) {
-          applied = nc - n.commit; papplied = applied;
-          n.commit = nc;
-        }
-      }
-      ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
-      break;
-    }
-    case RAFT_MSG_CLIENT_SET: {                                   // as client-set-handler 151-160
-      if (n.role != RAFT_LEADER) {
-        emit = 4;                                                 // redirect-client
-        break;
-      }
-      pkind = PLAN_ENTRY; ppoff = n.term; ppcnt = ma;
-      pold_base = n.base;
-      if (n.base + n.len != n.front) {
-        preloc = 1;
-        n.base = n.front;
-        n.front += n.len;
-      }
-      n.front += 1;
-      n.len += 1;
-      n.seq = 0;
-      appended = 1;
-      break;
-    }
-    case RAFT_MSG_VOTE_RESPONSE: {
-      if (mterm != n.term || !flag || n.role != RAFT_CANDIDATE) break;
-      const uint32_t votes = n.votes | 1u << src;
-      if (__popc(votes) < MAJ) {
-        n.votes = votes;
-        break;
-      }
-      n.role = RAFT_LEADER; n.votes = 0; n.lid = id;              // voted_for kept
-      n.lsp = 1; n.keys = peers;
-      nm = 1;
-      emit = 2;
-      elected = true;
-      break;
-    }
-    case RAFT_MSG_APPEND_RESPONSE: {
-      if (mterm != n.term || n.role != RAFT_LEADER) break;
-      if (!flag) {
-        nm = 3;
-        break;
-      }
-      nm = 4;
-      mchg = true;
-      // majority commit: the MAJ-th largest of {log_len} ∪ match_index (own slot holds log_len),
-      // by an unrolled compare-exchange network
-      int32_t vals[N];
-#pragma unroll
-      for (int p = 1; p <= N; ++p)
-        vals[p - 1] = p == (int)id ? (int32_t)n.len
-                                   : (p == (int)src ? (int32_t)mb : lsw.match(p - 1));
-#pragma unroll
-      for (int i = 1; i < N; ++i)
-#pragma unroll
-        for (int q = i; q > 0; --q)
-          if (vals[q - 1] < vals[q]) {
-            const int32_t tmp = vals[q]; vals[q] = vals[q - 1]; vals[q - 1] = tmp;
-          }
-      int32_t mm = vals[MAJ - 1];
-      if (mm > (int32_t)n.len) mm = (int32_t)n.len;
-      if (mm > (int32_t)n.commit && sar[(n.base + (uint32_t)mm - 1) % A].x == n.term) {
-        applied = (uint32_t)mm - n.commit; papplied = applied;
-        n.commit = (uint32_t)mm;
-      }
-      break;
-    }
-    default:
-      break;
-  }
-}
-
-// LDS words per wave: pair cells [cluster][sender][receiver other than the sender] of CELLW
-// words, then sender records [cluster][sender] of SRECW words, counters, and (Spec-Raft) the
-// wave's pre-tick arena frontiers.
-template <int N>
-constexpr int pair_words() { return (64 / N) * N * (N - 1) * CELLW; }
-template <int N>
-constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
-// NM_LDS: the wave's next_index / match_index rows live in LDS during a launch ([2][N][64]
-// words), for the N whose block then still fits four per CU.
-#ifndef RS_NM_LDS
-#define RS_NM_LDS 1
-#endif
-template <int N>
-constexpr bool nm_lds() { return RS_NM_LDS && N <= 5; }
-#ifdef RS_REGIONCOUNT   // diagnostic build: per-wave execution counts of code regions (RS_RC)
-constexpr int RC_WORDS = 32;
-#else
-constexpr int RC_WORDS = 0;
-#endif
-// TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key)
-constexpr int TRIP_WORDS = 64;
-template <int N, bool SPEC>
-constexpr int wave_lds_words() {
-  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
-         TRIP_WORDS + RC_WORDS;
-}
-template <int N, bool SPEC>
-constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
-}
-
-// SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
-// faithful kernel carries none of its code. One wave per workgroup: wave lifetimes differ by up
-// to 2x under load, and a multi-wave workgroup holds its CU slot and LDS until its slowest wave
-// ends (measured: 4-wave workgroups 1-2 % slower on C2/C3/C4).
-#ifndef RS_MIN_WAVES_PER_EU
-#define RS_MIN_WAVES_PER_EU 1
-#endif
-#ifndef RS_PACK_ACTIVITY   // 0: client-traffic launches packed by next event too (A/B builds)
-#define RS_PACK_ACTIVITY 1
-#endif
-#ifndef RS_DRAIN   // 0: no append-response drain (A/B builds)
-#define RS_DRAIN 1
-#endif
-
-// RAFT_SCHED_ALIGNED packing key of a node: its next event (deadline or queue head).
-__device__ __forceinline__ uint32_t sched_key_of(uint32_t deadline, const QueueR& rq,
-                                                 const QueueR& rs) {
-  return min(deadline, min(rq.arr, rs.arr));
-}
-// LITE: the launch has no client traffic, no faults and a fixed delay (DevSim::lite, set by the
-// host; C2): P0, client-set handling and redirects cannot occur, every emission takes the
-// fault-free delivery pack, and P3/P4 copy and compare one entry per memory round trip (they only
-// see host-written logs there). The compiler then drops that code: 121 -> ~100 VGPRs at N = 5.
-template <int N, bool TRACE, bool SPEC, bool LITE, bool CATCH = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_MIN_WAVES_PER_EU, 8)))
-tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
-  static_assert(!LITE || (!TRACE && !SPEC), "LITE is the plain faithful kernel");
-  static_assert(!CATCH || LITE, "catch-up launches follow the steady kernel (LITE only)");
-  constexpr int CPW = 64 / N;
-  constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
-  constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
+// The general tick kernel: one wave per workgroup (wave lifetimes differ by up to 2x under load,
+// and a multi-wave workgroup holds its CU slot and LDS until its slowest wave ends; measured:
+// 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound.
+template <int N, bool TRACE, bool SPEC, bool LITE>
+__global__ void __launch_bounds__(64) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int lane = threadIdx.x;
-  // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters and leader rows
-  unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
-  if (lane < 32) pw[lane] = S.client_pw[lane];
-  uint32_t* cells = smem + PW_WORDS;
-  uint32_t* lctr = cells + cell_words<N>();
-  uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
-  int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
-  if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
-  uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
-  tripsL[lane] = 0;          // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
-#ifdef RS_REGIONCOUNT
-  // region i executed by the wave (any lane active): the first active lane counts it
-  uint32_t* rcl = tripsL + TRIP_WORDS;
-  if (lane < RC_WORDS) rcl[lane] = 0;
-#define RS_RC(i)                                                       \
-  do {                                                                 \
-    if (lane == (int)__builtin_ctzll(__ballot(1))) rcl[i] += 1;        \
-  } while (0)
-#else
-#define RS_RC(i) do {} while (0)
-#endif
-  __builtin_amdgcn_wave_barrier();
-
-  // RAFT_SCHED_ALIGNED launches a grid sized for the padded packing; waves past its slots exit.
-  // A catch-up launch (S.resume: the steady kernel's bailed clusters) has a smaller grid whose
-  // waves take wave slots wave, wave + gridDim.x, ... in turn.
-  const uint32_t nslots = S.perm ? *S.nslots : S.C;
-  uint32_t wave = blockIdx.x;
-  if (CATCH && wave == 0 && lane == 0 && S.bail_report) *S.bail_report = nslots;
-  if (wave * CPW >= nslots) return;
-  do {
-    if (CATCH) tripsL[lane] = 0;
-    const int cs = lane / N, k0 = lane - cs * N;
-    const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
-    const uint32_t c0 = lane < CPW * N && slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
-    const bool active = c0 != INF;
-    const uint32_t c = active ? c0 : 0u;
-    const uint32_t gi = c * N + k0;
-    const uint32_t g = S.goff + c;
-    const int bl0 = (cs < CPW ? cs : 0) * N;     // the cluster's first lane
-    const uint32_t A = S.A;
-    constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
-    // this node's words in its cluster's block (field f at hp[f * N]) and the cluster's words
-    uint32_t* const hp = S.hot + (size_t)c * HB + k0;
-    uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
-
-    NodeR n = {};
-    uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
-    uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
-    if (active) {
-      const uint32_t fl = hp[HF_FLAGS * N], mk = hp[HF_MASKS * N], qm = hp[HF_QMETA * N];
-      n.role = fl & 3; n.vf = (fl >> 2) & 15; n.lid = (fl >> 6) & 15; n.fault = (fl >> 10) & 7;
-      n.seq = (fl >> 13) & 1; n.lsp = (fl >> 14) & 1;
-      n.votes = mk & 0xFFFF; n.keys = mk >> 16;
-      n.term = hp[HF_TERM * N]; n.commit = hp[HF_COMMIT * N]; n.len = hp[HF_LEN * N];
-      n.deadline = hp[HF_DEADLINE * N];
-      n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
-      n.rq.arr = hp[HF_REQ_ARR * N]; n.rs.arr = hp[HF_RES_ARR * N];
-      n.rq.tail = hp[HF_REQ_TAIL * N]; n.rs.tail = hp[HF_RES_TAIL * N];
-      n.base = hp[HF_ABASE * N]; n.front = hp[HF_AFRONT * N]; n.led = hp[HF_LED * N];
-      n.trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
-      hidx = hc[0]; hterm = hc[1]; hval = hc[2]; cnext = hc[3]; ccount = hc[4];
-      if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
-  #pragma unroll
-        for (int p = 0; p < N; ++p) {
-          nmL[p * 64 + lane] = hp[(HF_NEXT + p) * N];
-          nmL[(N + p) * 64 + lane] = hp[(HF_NEXT + N + p) * N];
-        }
-      }
-    }
-
-    // Per-cluster reductions over the cluster's N lanes (every lane of the wave must be active).
-    const uint32_t cmask = (1u << N) - 1;
-    auto cluster_min = [&](uint32_t x) {
-      uint32_t m = x;
-  #pragma unroll
-      for (int s = 0; s < N; ++s) m = min(m, (uint32_t)__shfl(x, bl0 + s));
-      return m;
-    };
-    auto cluster_any = [&](bool x) { return ((uint32_t)(__ballot(x) >> bl0) & cmask) != 0; };
-    const uint32_t tend = t0 + nt;
-    // Dead waves. A cluster whose every node is halted changes nothing but its client cursor and
-    // two counters from here on: a halt is permanent (D8) and a halted node drops what reaches it
-    // (core.clj:202-203), so its only events are client-sets into halted nodes (SIM_SPEC P0 + P2,
-    // to_halted). A wave holding only such clusters (the activity packing gives them waves of their
-    // own) runs their injections up to the launch's end here, one Philox draw each, with no trip;
-    // its trip loop then finds no event before tend. A wave that mixes live clusters in takes the
-    // trips (draining a dead cluster's injections there would stall its live wave mates).
-    if constexpr (!LITE && !SPEC) {
-      const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
-      if (S.client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
-        uint32_t cnt = 0;
-        while (active && cnext < tend) {
-          const uint4 d = philox(g, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
-          ++cnt;
-          ++ccount;
-          cnext = client_next_tick(cnext, d.w, pw, S.client_top, S.client_period, S.client_burst);
-        }
-        if (active && k0 == 0) {
-          lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
-          lctr_add(lctr, RAFT_CTR_TO_HALTED, cnt);
-        }
-      }
-    }
-
-    // Earliest tick at which any node of the lane's cluster can have an event (deadline, queue head
-    // or the next client-set), the same for all the cluster's lanes.
-    auto next_event = [&]() {
-      const uint32_t m = n.fault ? INF : min(n.deadline, min(n.rq.arr, n.rs.arr));
-      return cluster_min(active ? (LITE ? m : min(m, cnext)) : INF);
-    };
-  #ifdef RS_WAVELOG   // diagnostic build: per-wave start/end (100 MHz clock), active ticks, placement
-    const uint64_t wl_start = wall_clock64();
-    uint32_t wl_active = 0, wl_first = INF, wl_drain = 0, wl_inj = 0, wl_dead = 0;
-    {
-      const uint64_t fm = __ballot(active && n.fault);
-      const uint32_t all = (1u << N) - 1;
-      wl_dead = __popcll(__ballot(active && k0 == 0 && ((uint32_t)(fm >> bl0) & all) == all));
-    }
-    uint32_t wl_kmin = INF, wl_kmax = 0;
-    {
-      const uint32_t key = (active && k0 == 0 && S.skey) ? S.skey[c] : INF;
-      wl_kmin = wave_min(key);
-      wl_kmax = ~wave_min(key == INF ? ~0u : ~key);
-    }
-    // per-phase shader cycles summed over the wave's trips, stamped at wave-uniform points only:
-    // 0 P0, 3 P1, 4 P2, 5 P3, 6 P4, 7 the append-response drain, 8 the trip's loop head (next
-    // event, exit ballot); 9 the launch-start state load
-    uint32_t wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t wl_ts = 0;
-    const uint64_t wl_mt0 = __builtin_amdgcn_s_memtime();
-  #define RS_PHASE(i)                                          \
-    do {                                                       \
-      const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
-      wl_ph[i] += (uint32_t)(now_ - wl_ts);                    \
-      wl_ts = now_;                                            \
-    } while (0)
-  #else
-  #define RS_PHASE(i) do {} while (0)
-  #endif
-
-
-    // Every cluster keeps its own clock. Ticks before a cluster's next event change nothing for it
-    // (every handler, injection and delivery is keyed to a deadline, a queue head or the injection
-    // cursor), and clusters never interact, so each trip of the loop runs every cluster's next
-    // event tick -- not the wave's: a wave makes as many trips as its busiest cluster has event
-    // ticks, instead of the union of its clusters' event ticks (discrete-event skipping per
-    // cluster, tick-exact; Philox draws are keyed by the cluster's own tick).
-    // the cluster's first tick not yet simulated (catch-up: the tick it was bailed before)
-    uint32_t tnext = CATCH && active ? S.resume[slot] : t0;
-  #ifdef RS_WAVELOG
-    wl_ts = __builtin_amdgcn_s_memtime();
-    wl_ph[9] = (uint32_t)(wl_ts - wl_mt0);
-  #endif
-    for (;;) {
-      uint32_t t = max(tnext, next_event());
-      t = t < tend ? t : tend;
-      const bool on = active && t < tend;     // the cluster has a tick to run in this trip
-      if (!__ballot(on)) break;
-      if (!LITE && S.client_ppm) tripsL[lane] += on;
-      RS_RC(0);
-  #ifdef RS_WAVELOG
-      RS_PHASE(8);
-  #endif
-      const bool live = on && !n.fault;
-      // Opaque per-tick copies of the lane's indices: they keep the compiler from hoisting every
-      // address and shuffle index the active-tick phases use out of the tick loop, where each would
-      // hold a VGPR across all ticks (~50 VGPRs in all); recomputing them costs a few VALU per
-      // active tick.
-      uint32_t sgi = gi, sg = g;
-      int k = k0, bl = bl0;
-      asm volatile("" : "+v"(sgi), "+v"(sg), "+v"(k), "+v"(bl));
-      const uint32_t id = k + 1, peers = ALL & ~(1u << id);
-      uint32_t* const mycells = cells + bl * (N - 1) * CELLW;
-      uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
-      uint2* const sar = arena_of(S, sgi);
-      int32_t* const hnm = reinterpret_cast<int32_t*>(S.hot + (size_t)(sg - S.goff) * HB + k);
-      const PeerW lsw = nm_lds<N>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
-                                   : PeerW{hnm + HF_NEXT * N, hnm + (HF_NEXT + N) * N, (uint32_t)N};
-      if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
-        fr[lane] = n.front;
-        __builtin_amdgcn_wave_barrier();
-      }
-
-      // ---------------------------------------------------------- P0 client injection (D9, D14)
-      bool inj = false;
-      uint32_t injv = 0;
-      const bool cinj = !LITE && on && t == cnext;
-  #ifdef RS_WAVELOG
-      wl_inj += __ballot(cinj) ? 1 : 0;
-  #endif
-      if (!LITE && __ballot(cinj)) {
-        RS_RC(1);
-        if (cinj) {
-          const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
-          if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
-          if (1 + __umulhi(d.y, N) == id) {
-            inj = true;
-            injv = d.z;
-          }
-          ccount += 1;
-          cnext = client_next_tick(t, d.w, pw, S.client_top, S.client_period, S.client_burst);
-        }
-      }
-
-      // A client-set that lands in an empty REQ queue would be its head at arrival t, so it is
-      // kept in registers (dcs) instead of a global store + same-tick load; it is written to the
-      // queue only if this tick's alts!! choice takes the RES queue instead.
-      bool dcs = false;
-      if (!LITE && __ballot(inj)) {
-        if (inj) {
-          if (live && n.rq.c == 0) dcs = true;
-          else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                       make_uint4(0, 0, 0, 0), lctr);
-        }
-      }
-
-      RS_PHASE(0);
-      // ---------------------------------------------------------------- P1 one event per node
-      const bool req_ok = live && (dcs || n.rq.arr <= t);
-      const bool res_ok = live && n.rs.arr <= t;
-      uint32_t sentmask = 0;
-      // P3 plan: PAYLOAD copies ppcnt entries from psrc's arena slot ppoff, ENTRY appends the
-      // entry (ppoff, ppcnt) = (term, val); the old log starts at pold_base and (preloc) is first
-      // moved to the node's new base. The old length (n.len - entries added) and the first applied
-      // position (n.commit - papplied) are derived in P3 rather than held across P2.
-      uint32_t pkind = PLAN_NONE, psrc = 1, ppoff = 0, ppcnt = 0, pold_base = 0, preloc = 0,
-               papplied = 0;
-      bool elected = false, mchg = false;
-      uint32_t pmax = 0;                                        // largest AE payload emitted
-      uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
-      if (live && (req_ok || res_ok || t >= n.deadline)) {
-        RS_RC(2);
-        // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
-        // and for the next timeout of a non-leader (core.clj:174); leaders' events skip it.
-        uint4 w = make_uint4(0, 0, 0, 0);
-        bool have_w = false;
-        int which = -1;
-        if (req_ok && res_ok) {
-          RS_RC(4);
-          w = event_draw(sg, id, t, S);
-          have_w = true;
-          which = (w.x & 1) ? 1 : 0;
-        } else if (req_ok) {
-          which = 0;
-        } else if (res_ok) {
-          which = 1;
-        }
-        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
-        if (dcs) {
-          if (which == 0) {
-            m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
-            lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
-          } else {
-            qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                    make_uint4(0, 0, 0, 0), lctr);
-          }
-        }
-        if (which >= 0 && !(dcs && which == 0)) {
-          // Take the queue head (qpop): both loads are issued first, and a non-leader's EVENT draw
-          // (needed for its next timeout whatever the message does, unless it becomes leader) is
-          // computed in their shadow. The next head's arrival is loaded unconditionally (a slot of
-          // the ring is always in bounds) and used only when the queue stays non-empty.
-          RS_RC(3);
-          const QueueR q = which ? n.rs : n.rq;
-          const uint32_t* qb = qslots(S, sgi, which);
-          const size_t qs = qstride(S, which);
-          const uint4* sp = reinterpret_cast<const uint4*>(qb + q.h * qs);
-          m0 = sp[0];
-          m1 = sp[1];
-          const uint32_t nh = wrapq(q.h + 1, S.Q);
-          // Only a queue that stays non-empty has a next head. Its arrival is known without a load
-          // when one message remains or all queued ones share the head's arrival (the queue is
-          // sorted, so head == tail means all equal): then nothing this tick waits on memory.
-          uint32_t narr = INF;
-          if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
-          if (!have_w && n.role != RAFT_LEADER) {
-            RS_RC(5);
-            w = event_draw(sg, id, t, S);
-            have_w = true;
-          }
-          QueueR r = q;
-          r.h = nh;
-          r.c -= 1;
-          r.arr = r.c ? narr : INF;
-          r.tail = r.c ? r.tail : 0u;
-          // A queue that drains restarts its ring at slot 0 (the ring position is not state: reads
-          // linearise from the head). Steady-state traffic then lands in slots 0..P-1, where a
-          // cluster's nodes are adjacent, instead of walking all Q slots of the [slot][node] layout.
-          if (!r.c) r.h = 0;
-          if (which) n.rs = r;
-          else n.rq = r;
-        }
-        const uint32_t hdr = m0.y, mterm = m0.z, ma = m0.w, mb = m1.x, met = m1.y, mev = m1.z,
-                       mpoff = m1.w;
-  #ifdef RS_WAVELOG
-        asm volatile("" ::"v"(hdr), "v"(mb));   // the pop's wait lands before the stamp
-  #endif
-        const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
-                       mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
-        if constexpr (TRACE) {
-          const uint32_t tes = S.tecount[sgi];
-          trace_record<N>(S, sgi, t, n, lsw, m0, m1, tes);
-          if (which >= 0 && type == RAFT_MSG_APPEND_ENTRIES && pcnt) {
-            tr_cnt = pcnt; tr_src = src; tr_poff = mpoff; tr_at = tes;
-            S.tecount[sgi] = tes + pcnt;
-          }
-        }
-
-        // Every throw site of the reference precedes every mutation of its handler (SIM_SPEC D8),
-        // so each case decides `fault` first and only then updates the node in place.
-        uint32_t fault = 0, ev = 0;
-        // 1 request-vote bcast, 2 append-entries bcast, 3 one reply, 4 redirect-client
-        int emit = 0;
-        int nm = 0;                   // next/match: 1 init, 2 clear, 3 dec next[src], 4 set src
-        uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);  // reply cell words
-        uint32_t appended = 0, applied = 0;
-        const bool was_leader = n.role == RAFT_LEADER;
-        bool rearm = false;           // SPEC: the event resets the election timer (SIM_SPEC §8)
-
-        if constexpr (SPEC) {
-          spec_handle<N, MAJ>(S, n, lsw, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
-                              emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
-                              pold_base, preloc, papplied, elected, mchg, rearm);
-        } else if (which < 0) {
-          RS_RC(7);
-          if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
-            ev = 7;
-            // append-entries-rpc (core.clj:56-67): last-entry, then per peer in doseq order
-            // (- nil 1) and subvec of a LazySeq
-            const uint32_t first = id == 1 ? 2u : 1u;
-            if (n.commit > n.len) fault = RAFT_FAULT_IOOBE;
-            else if (!n.lsp || !((n.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
-            else if (n.seq) fault = RAFT_FAULT_CCE;
-            else if ((n.keys & peers) != peers) fault = RAFT_FAULT_NPE;
-            else emit = 2;
-          } else {                                            // timeout-handler 166-169
-            ev = 6;
-            if (n.commit > n.len) {                           // last-entry (log.clj:47-49)
-              fault = RAFT_FAULT_IOOBE;
-            } else {
-              uint32_t ep = 0, et = 0, evl = 0;
-              if (n.commit) {
-                const uint2 e = sar[(n.base + n.commit - 1) % A];
-                ep = 1; et = e.x; evl = e.y;
-              }
-              n.role = RAFT_CANDIDATE; n.vf = id; n.votes = 1u << id; n.term += 1;  // 69-73
-              ra = make_uint4(RAFT_MSG_REQUEST_VOTE | id << 3 | ep << 8, n.term, n.commit, 0);
-              rb = make_uint4(et, evl, 0, 0);
-              emit = 1;
-            }
-          }
-        } else {
-          RS_RC(8);
-          ev = type;
-          switch (type) {
-            case RAFT_MSG_REQUEST_VOTE: {                     // request-vote-handler 91-103
-              uint32_t consistent = 1;
-              if (!(S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) && ma != 0) {
-                if (ma > n.len) {
-                  fault = RAFT_FAULT_IOOBE;
-                  break;
-                }
-                const uint2 e = sar[(n.base + ma - 1) % A];
-                consistent = mep && e.x == met && e.y == mev;
-              }
-              const uint32_t grant = mterm >= n.term && n.vf == 0 && consistent;
-              ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
-              if (grant) n.vf = src;
-              emit = 3;
-              break;
-            }
-            case RAFT_MSG_APPEND_ENTRIES: {                   // append-entries-handler 105-123
-              uint32_t consistent = 1;
-              if (mb != 0) {
-                if (mb > n.len) {
-                  fault = RAFT_FAULT_IOOBE;
-                  break;
-                }
-                const uint2 e = sar[(n.base + mb - 1) % A];
-                consistent = mep && e.x == met && e.y == mev;
-              }
-              if (mterm < n.term) {
-                ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
-              } else if (!consistent) {
-                ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
-                n.len = n.len > mb ? n.len - mb : 0;          // remove-from! 78-81
-                n.seq = 1;
-              } else {
-                if (n.len + pcnt > S.L) {
-                  fault = RAFT_FAULT_OVERFLOW;
-                  break;
-                }
-                ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3 | 1u << 7, n.term, ma, mb + pcnt);
-                pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff; ppcnt = pcnt;
-                pold_base = n.base;
-                if (pcnt) {                                    // append-entries! 61-64
-                  if (n.base + n.len != n.front) {
-                    preloc = 1;
-                    n.base = n.front;
-                    n.front += n.len;
-                  }
-                  n.front += pcnt;
-                          }
-                const uint32_t oldc = n.commit;
-                n.len += pcnt;
-                n.seq = 0;
-                appended = pcnt;
-                n.commit = n.len;                              // apply-entries! 69-76
-                applied = n.commit > oldc ? n.commit - oldc : 0;
-                papplied = applied;
-                n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;  // candidate->follower 75-78
-                n.lid = src; n.term = mterm;
-              }
-              emit = 3;
-              break;
-            }
-            case RAFT_MSG_CLIENT_SET: {                        // client-set-handler 151-160
-              if (LITE) break;                                 // (no client traffic)
-              if (n.role != RAFT_LEADER) {                     // redirect-client: no state change
-                emit = 4;
-                break;
-              }
-              if (n.len + 1 > S.L) {
-                fault = RAFT_FAULT_OVERFLOW;
-                break;
-              }
-              pkind = PLAN_ENTRY; ppoff = n.term; ppcnt = ma;
-              pold_base = n.base;
-              if (n.base + n.len != n.front) {
-                preloc = 1;
-                n.base = n.front;
-                n.front += n.len;
-              }
-              n.front += 1;
-                    n.len += 1;
-              n.seq = 0;
-              appended = 1;
-              break;
-            }
-            case RAFT_MSG_VOTE_RESPONSE: {                     // vote-response-handler 125-139
-              if (n.commit > n.len) {                          // last-entry first
-                fault = RAFT_FAULT_IOOBE;
-                break;
-              }
-              if (mterm > n.term) {
-                n.term = mterm;
-                n.role = RAFT_FOLLWER; n.vf = 0; n.votes = 0;
-              } else if (flag && n.role == RAFT_CANDIDATE) {
-                const uint32_t votes = n.votes | 1u << src;
-                if (__popc(votes) < (N + 1) / 2) {             // majority? 19-21
-                  n.votes = votes;
-                } else if (n.seq) {
-                  fault = RAFT_FAULT_CCE;      // append-entries-rpc's entries-from (log.clj:53)
-                } else {                                       // candidate->leader 80-84
-                  n.role = RAFT_LEADER; n.vf = 0; n.votes = 0; n.lid = id;
-                  n.lsp = 1; n.keys = peers;                   // leader-state 40-42
-                  nm = 1;
-                  emit = 2;
-                  elected = true;
-                }
-              }
-              break;
-            }
-            case RAFT_MSG_APPEND_RESPONSE: {                   // append-response-handler 141-149
-              if (mterm > n.term) {                            // leader->follower 86-89
-                n.term = mterm;
-                n.role = RAFT_FOLLOWER; n.lid = 0; n.lsp = 0; n.keys = 0;
-                nm = 2;
-              } else if (!flag) {
-                if (!n.lsp || !((n.keys >> src) & 1)) {
-                  fault = RAFT_FAULT_NPE;                      // (dec nil)
-                  break;
-                }
-                nm = 3;
-              } else {
-                n.lsp = 1;
-                n.keys |= 1u << src;
-                nm = 4;
-                mchg = true;
-              }
-              break;
-            }
-            default:
-              break;
-          }
-        }
-        const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
-        if (fault) {                                   // D8: halted with the pre-event state
-          RS_RC(9);
-          n.fault = fault;
-          n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, fault);
-          lctr_add(lctr, RAFT_CTR_HALT_IOOBE + fault - 1, 1);
-          pkind = PLAN_NONE;
-          papplied = 0;
-          elected = false;
-          mchg = false;
-        } else {
-          // generate-timeout (core.clj:171-174) for the next wait: every event re-arms the timer
-          // (D4); Spec-Raft keeps Raft's timers (SIM_SPEC §8)
-          if (n.role == RAFT_LEADER) {
-            if (!SPEC || ev == 7 || elected) n.deadline = t + S.hb;
-          } else if (!SPEC || ev == 6 || rearm || was_leader) {
-            if (!have_w) RS_RC(6);
-            if (!have_w) w = event_draw(sg, id, t, S);
-            have_w = true;
-            n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
-          }
-          RS_RC(10);
-          n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
-          // leader-state words (cold, in HBM)
-          if (nm == 1 || nm == 2) {
-            const int32_t first_next = (int32_t)((SPEC ? n.len : n.commit) + 1);
-  #pragma unroll
-            for (int p = 1; p <= N; ++p) {
-              lsw.next(p - 1) = (nm == 1 && p != (int)id) ? first_next : 0;
-              lsw.match(p - 1) = 0;
-            }
-          } else if (nm == 3) {
-            if constexpr (SPEC) {
-              const int32_t nx = lsw.next(src - 1) - 1;
-              lsw.next(src - 1) = nx > 1 ? nx : 1;
-            } else {
-              lsw.next(src - 1) -= 1;
-            }
-          } else if (nm == 4) {
-            lsw.next(src - 1) = (int32_t)(SPEC ? mb + 1 : mb);
-            lsw.match(src - 1) = (int32_t)(SPEC ? mb : ma);
-          }
-          lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
-          lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
-          lctr_add(lctr, RAFT_CTR_ENTRIES_APPLIED, applied);
-          if (elected) {
-            lctr_add(lctr, RAFT_CTR_LEADERS, 1);
-            n.led = n.term;
-          }
-          // ------------------------------------------------ redirect-client (server.clj:62-63)
-          // to the :leader-id, else (rand-nth cluster) by w2 of the EVENT draw (core.clj:153-155);
-          // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
-          // {a, b + 1} arriving at t + 1 outside the fault model. A redirect to the node itself
-          // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
-          if (!LITE && emit == 4) {
-            RS_RC(11);
-            emit = 0;
-            if (mb >= S.client_redirects) {
-              lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
-            } else {
-              uint32_t dst = n.lid;
-              if (!dst) {
-                if (!have_w) w = event_draw(sg, id, t, S);
-                const uint32_t i = __umulhi(w.z, N - 1);
-                dst = i + 1 < id ? i + 1 : i + 2;
-              }
-              lctr_add(lctr, RAFT_CTR_REDIRECTS, 1);
-              *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
-                  make_uint2(dst == id ? mb + 1 : 0u, ma);
-              if (dst != id) {
-                uint32_t* cl =
-                    mycells + (k * (N - 1) + (dst - 1 < (uint32_t)k ? dst - 1 : dst - 2)) * CELLW;
-                cell_put(cl, make_uint4(RAFT_MSG_CLIENT_SET, 0, 0, mb + 1), make_uint4(0, 0, 0, 0));
-                cl[CELLW - 1] = 1u | 1u << 16;
-              }
-              sentmask |= 1u << dst;
-            }
-          }
-          // ------------------------------------------------ emission (rpc / respond)
-          if (emit) {
-            RS_RC(12);
-            bool part = false;
-            uint32_t sides = 0;
-            if (!LITE && S.part_ppm) {
-              const uint4 pw = philox(sg, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
-              part = ppm(pw.x) < S.part_ppm;
-              sides = pw.y;
-            }
-            *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
-                emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
-            if (emit == 3) {
-              RS_RC(13);
-              uint32_t* cl =
-                  mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
-              cell_put(cl, ra, rb);
-              lctr_add(lctr, RAFT_CTR_SENT, 1);
-              transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
-            } else {
-              RS_RC(14);
-              // Message words first, for every peer at once: the next-index loads (and then the
-              // prev-entry loads) of all peers are independent, so they overlap instead of paying
-              // one memory round trip per peer; the fault draws follow in a compact loop.
-              int32_t nxs[N];
-  #pragma unroll
-              for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? lsw.next(p) : 0;
-  #pragma unroll 1
-              for (int p = 1; p <= N; ++p) {
-                if (p == (int)id) continue;
-                if (SPEC && emit == 2) {                    // SIM_SPEC §8 broadcast
-                  const int32_t pv = nxs[p - 1] - 1;
-                  const uint32_t prev = pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
-                  uint32_t ep = 0, et = 0, evl = 0;
-                  if (prev) {
-                    const uint2 e = sar[(n.base + prev - 1) % A];
-                    ep = 1; et = e.x; evl = e.y;
-                  }
-                  const uint32_t pc = n.len - prev;
-                  pmax = pc > pmax ? pc : pmax;
-                  ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
-                                  n.commit, prev);
-                  rb = make_uint4(et, evl, pc ? n.base + prev : 0, 0);
-                } else if (emit == 2) {
-                  const int32_t nx = nxs[p - 1];
-                  const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
-                  const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
-                  uint32_t ep = 0, et = 0, evl = 0, pc = 0, po = 0;
-                  if (start < n.len) {
-                    const uint2 e = sar[(n.base + start) % A];
-                    ep = 1; et = e.x; evl = e.y;
-                    pc = n.len - start - 1;
-                    po = pc ? n.base + start + 1 : 0;
-                  }
-                  pmax = pc > pmax ? pc : pmax;
-                  ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
-                                  n.commit, (uint32_t)prev);
-                  rb = make_uint4(et, evl, po, 0);
-                }
-                cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
-              }
-              if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
-              lctr_add(lctr, RAFT_CTR_SENT, N - 1);
-              if constexpr (LITE) {          // every peer gets one copy after the fixed delay
-  #pragma unroll
-                for (int j = 0; j < N - 1; ++j)
-                  mycells[(k * (N - 1) + j) * CELLW + CELLW - 1] = S.dmin | 1u << 16;
-                sentmask |= peers;
-              } else {
-  #pragma unroll 1
-                for (int p = 1; p <= N; ++p) {
-                  if (p == (int)id) continue;
-                  transmit<N, LITE>(S, sg, t, id, p, part, sides,
-                              mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW,
-                              sentmask, lctr);
-                }
-              }
-            }
-          }
-        }
-      }
-
-      RS_PHASE(3);
-      // ---------------------------------------------------------------- P2 network delivery
-      if (__ballot(sentmask != 0)) {
-        RS_RC(16);
-        // Senders that addressed this lane this tick (one ds_bpermute per cluster slot), then one
-        // copy per loop trip in (sender id, copy) order: a single qinsert call site for the wave.
-        uint32_t inmask = 0;
-  #pragma unroll
-        for (int s = 0; s < N; ++s) {
-          const uint32_t sm = __shfl(sentmask, bl + s);
-          inmask |= ((sm >> id) & 1u) << s;
-        }
-        if (!on) inmask = 0;
-        uint32_t copy = 0;
-        while (inmask) {
-          RS_RC(17);
-          const int s = __builtin_ctz(inmask);
-          const uint2 sr = *reinterpret_cast<const uint2*>(mysrec + s * SRECW);
-          uint2 c0 = make_uint2(RAFT_MSG_CLIENT_SET, sr.x), c1 = make_uint2(0, 0),
-                c2 = make_uint2(0, 1u | 1u << 16);           // a redirect to this node itself
-          if (s != k) {
-            const uint2* cl = reinterpret_cast<const uint2*>(
-                mycells + (s * (N - 1) + (k < s ? k : k - 1)) * CELLW);
-            c0 = cl[0]; c1 = cl[1]; c2 = cl[2];
-          }
-          const uint32_t d = (LITE || copy == 0) ? (c2.y & 0xFF) : ((c2.y >> 8) & 0xFF);
-          const int which = (c0.x & 7) <= RAFT_MSG_CLIENT_SET ? 0 : 1;
-          QueueR q = which ? n.rs : n.rq;
-          const uint4 q0 = make_uint4(t + d, c0.x, s != k ? sr.x : 0u, sr.y),
-                      q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
-          qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
-          if (which) n.rs = q;
-          else n.rq = q;
-          if (LITE || ++copy >= (c2.y >> 16)) {   // LITE: one copy per message
-            copy = 0;
-            inmask &= inmask - 1;
-          }
-        }
-      }
-
-      RS_PHASE(4);
-      // ---------------------------------------------------------------- P3 log writes
-      // m entries were added at position n.len - m (appended_at, -1 when none)
-      const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
-      const int appended_at = m ? (int)(n.len - m) : -1;
-      if (__ballot(m || papplied || (TRACE && tr_cnt))) {
-        RS_RC(19);
-        const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
-        if (m) {
-          const uint32_t pold_len = n.len - m;
-          // physical slots advance with a wrap instead of a per-entry modulo
-          if (preloc)
-            arena_copy<LITE ? 1 : RS_COPY_BATCH>(sar, n.base % A, sar, pold_base % A, pold_len, A);
-          uint32_t di = (n.base + pold_len) % A;
-          if (pkind == PLAN_ENTRY) {
-            sar[di] = make_uint2(ppoff, ppcnt);
-          } else {
-            // entries i with sender frontier > poff + i + A were overwritten (SIM_SPEC P3)
-            const int64_t ev = (int64_t)sfront - (int64_t)A - (int64_t)ppoff;
-            const uint32_t evicted = ev <= 0 ? 0u : (ev >= (int64_t)m ? m : (uint32_t)ev);
-            const uint2* sa = arena_of(S, sgi - k + psrc - 1);
-            uint32_t si = (ppoff + evicted) % A;
-            for (uint32_t i = 0; i < evicted; ++i) {
-              sar[di] = make_uint2(0, 0);
-              di = di + 1 == A ? 0 : di + 1;
-            }
-            arena_copy<LITE ? 1 : RS_COPY_BATCH>(sar, di, sa, si, m - evicted, A);
-            lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
-          }
-        }
-        if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
-          RS_RC(21);
-          uint32_t cc = S.ccount[sgi];
-          uint32_t si = (n.base + n.commit - papplied) % A;
-          for (uint32_t i = 0; i < papplied; ++i, ++cc) {
-            if (S.SC) S.stream[(size_t)sgi * S.SC + cc % S.SC] = sar[si].y;
-            si = si + 1 == A ? 0 : si + 1;
-          }
-          S.ccount[sgi] = cc;
-        }
-        if constexpr (TRACE) {   // the traced message's :entries, resolved like the payload above
-          const uint32_t tfront = __shfl(n.front, bl + (int)tr_src - 1);
-          if (tr_cnt && S.TE) {
-            const int64_t ev = (int64_t)tfront - (int64_t)A - (int64_t)tr_poff;
-            const uint32_t evicted = ev <= 0 ? 0u : (ev >= (int64_t)tr_cnt ? tr_cnt : (uint32_t)ev);
-            const uint2* sa = arena_of(S, sgi - k + tr_src - 1);
-            uint2* ring = S.tent + (size_t)sgi * S.TE;
-            for (uint32_t i = 0; i < tr_cnt; ++i)
-              ring[(tr_at + i) % S.TE] =
-                  i < evicted ? make_uint2(0, 0) : sa[(tr_poff + i) % A];
-          }
-        }
-      }
-
-      RS_PHASE(5);
-      // ---------------------------------------------------------------- P4 invariant checker
-      // the majority-match scan can raise hwm only when the leader's log reaches past it
-      const bool mcheck = (elected || mchg) && n.len > hidx;
-      if (__ballot(elected || appended_at >= 0 || mcheck)) {
-        RS_RC(22);
-        if (__ballot(elected)) {                       // election safety
-          bool bad = false;
-  #pragma unroll
-          for (int s = 0; s < N; ++s) {
-            const uint32_t ls = __shfl(n.led, bl + s);
-            bad |= elected && s != k && ls == n.led;
-          }
-          if (bad) violation(lctr, RAFT_CTR_VIOL_ELECTION, t);
-        }
-        if (__ballot(appended_at >= 0)) {              // log matching
-          RS_RC(23);
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
-          bool bad = false;
-  #pragma unroll
-          for (int s = 0; s < N; ++s) {
-            const uint32_t sb = __shfl(n.base, bl + s), sl = __shfl(n.len, bl + s);
-            if (appended_at >= 0 && s != k && !bad) {
-              const uint2* oa = arena_of(S, sgi - k + s);
-              const uint32_t hi = n.len < sl ? n.len : sl, lo = (uint32_t)appended_at;
-              if (hi > lo)
-                bad = log_conflict<LITE ? 1 : 4>(sar, (n.base + lo) % A, oa, (sb + lo) % A, hi - lo, A);
-            }
-          }
-          if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
-        }
-        if (elected && hidx > 0) {                     // leader completeness (pre-tick hwm)
-          bool ok = n.len >= hidx;
-          if (ok) {
-            const uint2 e = sar[(n.base + hidx - 1) % A];
-            ok = e.x == hterm && e.y == hval;
-          }
-          if (!ok) violation(lctr, RAFT_CTR_VIOL_COMPLETE, t);
-        }
-        int32_t cm = -1;
-        uint32_t ct = 0, cv = 0;
-        if (on && n.role == RAFT_LEADER && mcheck) {
-          int32_t vals[N];
-          vals[0] = (int32_t)n.len;
-          int j = 1;
-  #pragma unroll
-          for (int p = 1; p <= N; ++p) {
-            if (p == (int)id) continue;
-            vals[j++] = ((n.keys >> p) & 1) ? lsw.match(p - 1) : 0;
-          }
-  #pragma unroll
-          for (int i = 1; i < N; ++i)
-  #pragma unroll
-            for (int q = i; q > 0; --q)
-              if (vals[q - 1] < vals[q]) {
-                const int32_t tmp = vals[q]; vals[q] = vals[q - 1]; vals[q - 1] = tmp;
-              }
-          int32_t mm = vals[MAJ - 1];
-          if (mm > (int32_t)n.len) mm = (int32_t)n.len;
-          if (mm > (int32_t)hidx) {
-            const uint2 e = sar[(n.base + (uint32_t)mm - 1) % A];
-            if (!SPEC || e.x == n.term) {   // SIM_SPEC §8: committed only in the leader's term
-              cm = mm;
-              ct = e.x; cv = e.y;
-            }
-          }
-        }
-        if (__ballot(cm >= 0)) {                       // cluster argmax, lowest id on ties
-          int32_t best = -1;
-          uint32_t bt = 0, bv = 0;
-  #pragma unroll
-          for (int s = 0; s < N; ++s) {
-            const int32_t sm = __shfl(cm, bl + s);
-            const uint32_t st = __shfl(ct, bl + s), sv = __shfl(cv, bl + s);
-            if (sm > best) { best = sm; bt = st; bv = sv; }
-          }
-          if (on && best > 0) { hidx = (uint32_t)best; hterm = bt; hval = bv; }
-        }
-      }
-      RS_PHASE(6);
-  #ifdef RS_WAVELOG
-      ++wl_active;
-      wl_first = wl_first == INF ? t - t0 : wl_first;
-  #endif
-
-      // ------------------------------------------------------- append-response drain (faithful)
-      // A leader answers each append-response with no message, no log write and -- while its log
-      // does not reach past the checker's high-water mark -- no check: the event touches its own
-      // words only (core.clj:141-149, timer 171-174). Ticks at which a cluster's only events are
-      // such responses are therefore run here without P0 and P2-P4, one response per leader per
-      // tick as above, until the cluster's next other event E (the REQ head and client-set of every
-      // node, and the deadline and RES head of every node that is not a live leader). A tick at
-      // which a leader's event is anything else (a heartbeat, or a head message that is not such
-      // a response) ends the cluster's drain before that tick; the loop above then runs it. Steady
-      // state: a heartbeat round's four responses at the leader take one trip through here, not four ticks.
-      // Only where it pays: clusters of up to five nodes without client traffic (C2; with client
-      // traffic a cluster has an event nearly every tick of a burst: measured C3 +3 % with one
-      // wave-wide clock, unchanged with per-cluster clocks, C4-N9 +1 %), and it would cost the
-      // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
-      if constexpr (RS_DRAIN && !SPEC && !TRACE && N <= 5) if (LITE || !S.client_ppm) {
-        // leaders whose responses can drain: a log past the hwm makes a success response a
-        // checker event (C3/C4 replication), so those leaders stay with the loop
-        const bool elig = on && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
-        if (__ballot(elig && n.rs.c)) {
-          const uint32_t oth = (!on || n.fault) ? INF
-                               : elig ? min(n.rq.arr, cnext)
-                                      : min(min(n.deadline, n.rq.arr), min(n.rs.arr, cnext));
-          // the cluster's next other event E; a cluster drains while its leaders' responses are
-          // its only events before E
-          const uint32_t E = min(cluster_min(oth), tend);
-          const bool any_res = cluster_any(elig && n.rs.c);
-          const bool any_ready = cluster_any(elig && n.rs.arr < E);
-          bool dr = on && any_res && any_ready && E > t + 1;
-          if (__ballot(dr)) {
-            RS_RC(25);
-            const uint32_t* qb = qslots(S, sgi, 1);
-            const size_t qs = qstride(S, 1);
-            // A cluster with one eligible leader (the usual case) drains in that lane alone: its
-            // ticks are the leader's own, so the loop needs no cluster reductions per tick. The
-            // stop rules are the cluster loop's below: tau reaches E, a heartbeat falls due, or the
-            // head message is not such a response.
-            const uint32_t em = (uint32_t)(__ballot(elig) >> bl0) & cmask;
-            const bool solo = dr && __popc(em) == 1;
-            if (__ballot(solo)) {
-              if (solo && elig) {
-                for (;;) {
-                  const uint32_t tau = max(min(n.rs.arr, n.deadline), t + 1);
-                  if (tau >= E || n.rs.arr > tau) break;       // E, or the heartbeat's tick
-                  const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
-                  const uint4 m0 = sp[0], m1 = sp[1];
-                  const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
-                  uint32_t narr = INF;
-                  if (n.rs.c > 1)
-                    narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
-                  const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15,
-                                 flag = (hdr >> 7) & 1;
-                  if (!((hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
-                        (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1))))
-                    break;
-                  QueueR r = n.rs;
-                  r.h = nh;
-                  r.c -= 1;
-                  r.arr = r.c ? narr : INF;
-                  r.tail = r.c ? r.tail : 0u;
-                  if (!r.c) r.h = 0;
-                  n.rs = r;
-                  if (flag) {                                // append-response-handler 145-149
-                    n.lsp = 1;
-                    n.keys |= 1u << src;
-                    lsw.next(src - 1) = (int32_t)m1.x;
-                    lsw.match(src - 1) = (int32_t)m0.w;
-                  } else {                                   // 143-144: (dec next-index)
-                    lsw.next(src - 1) -= 1;
-                  }
-                  n.deadline = tau + S.hb;
-                  n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
-                                        n.term, 0);
-                  lctr_add(lctr, RAFT_CTR_EV_AR, 1);
-                  t = tau;
-                }
-              }
-              const uint32_t lt = __shfl(t, bl0 + (em ? (int)__builtin_ctz(em) : 0));
-              if (solo) t = lt;                              // the cluster takes the leader's clock
-              dr = dr && !solo;
-            }
-            for (;;) {
-              const uint32_t nxt = elig ? min(n.rs.arr, n.deadline) : INF;   // leader's next event
-              const uint32_t tau = max(cluster_min(nxt), t + 1);
-              dr = dr && tau < E;
-              const bool ev = dr && elig && n.rs.arr <= tau;  // a ready message beats the timer
-              const bool hbeat = dr && elig && !ev && n.deadline <= tau;
-              uint4 m0 = make_uint4(0, 0, 0, 0), m1 = make_uint4(0, 0, 0, 0);
-              uint32_t narr = INF;
-              const uint32_t nh = wrapq(n.rs.h + 1, S.Q);
-              if (ev) {
-                const uint4* sp = reinterpret_cast<const uint4*>(qb + n.rs.h * qs);
-                m0 = sp[0];
-                m1 = sp[1];
-                if (n.rs.c > 1)
-                  narr = (n.rs.c == 2 || n.rs.arr == n.rs.tail) ? n.rs.tail : qb[nh * qs];
-              }
-              const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
-              const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
-                                  (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
-              // a tick at which any node of the cluster needs the loop above is the loop's to run
-              dr = dr && !cluster_any(hbeat || (ev && !simple));
-              if (!__ballot(dr)) break;
-              RS_RC(26);
-              if (dr && ev) {
-                QueueR r = n.rs;
-                r.h = nh;
-                r.c -= 1;
-                r.arr = r.c ? narr : INF;
-                r.tail = r.c ? r.tail : 0u;
-                if (!r.c) r.h = 0;
-                n.rs = r;
-                if (flag) {                                  // append-response-handler 145-149
-                  n.lsp = 1;
-                  n.keys |= 1u << src;
-                  lsw.next(src - 1) = (int32_t)m1.x;
-                  lsw.match(src - 1) = (int32_t)m0.w;
-                } else {                                     // 143-144: (dec next-index)
-                  lsw.next(src - 1) -= 1;
-                }
-                n.deadline = tau + S.hb;
-                n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
-                                      n.term, 0);
-                lctr_add(lctr, RAFT_CTR_EV_AR, 1);
-              }
-              if (dr) t = tau;
-  #ifdef RS_WAVELOG
-              ++wl_drain;
-  #endif
-            }
-          }
-        }
-      }
-      RS_PHASE(7);
-      tnext = t + 1;
-    }
-  #ifdef RS_REGIONCOUNT
-    __builtin_amdgcn_wave_barrier();
-    if (lane < RC_WORDS && S.wavelog) S.wavelog[(size_t)wave * 32 + lane] = rcl[lane];
-  #endif
-  #ifdef RS_WAVELOG
-    if (lane == 0 && S.wavelog) {
-      const uint64_t wl_end = wall_clock64();
-      uint32_t hw, xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 32);
-      rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
-                          (uint32_t)(wl_end >> 32));
-      rec[1] = make_uint4(wl_active, hw, xcc, (wl_kmax - wl_kmin) << 16 | (wl_first & 0xFFFF));
-      rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
-      rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
-      rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
-      rec[5] = make_uint4(wl_drain, wl_inj, wl_dead, 0);
-    }
-  #endif
-
-    // ---------------------------------------------------------------- write back
-    if (S.shist) {
-      // RAFT_SCHED_ALIGNED: the cluster's packing key relative to the next launch, counted into the
-      // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
-      const uint32_t me = active && !n.fault ? sched_key_of(n.deadline, n.rq, n.rs) : INF;
-      uint32_t cm = active ? cnext : INF;
-  #pragma unroll
-      for (int s = 0; s < N; ++s) cm = min(cm, (uint32_t)__shfl(me, bl0 + s));
-      const bool head = active && k0 == 0;
-      // With client traffic every cluster is busy on most ticks of a burst and a wave lasts as
-      // long as its busiest cluster (per-cluster clocks): clusters are then packed by how many
-      // event ticks they ran in this launch, busiest first (they start first and are done before
-      // the tail), instead of by their next event.
-      // The last bucket is kept for dead clusters (every node halted), which the next launch then
-      // packs into waves of their own and runs without trips (below the state load).
-      const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
-      const uint32_t key = !head ? INF
-                           : RS_PACK_ACTIVITY && S.client_ppm
-                               ? (dead ? SCHED_BUCKETS - 1
-                                       : SCHED_BUCKETS - 2 - min(tripsL[lane], SCHED_BUCKETS - 2))
-                               : sched_bucket(cm, tend);
-      if (head) S.skey[c] = key;
-      // a packed wave's clusters usually share their next key: one histogram atomic for the wave
-      const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
-      const uint32_t heads = (uint32_t)__popcll(__ballot(head));   // (ballot outside any branch)
-      if (kmin == kmax) {
-        if (lane == 0 && kmin != INF) atomicAdd(&S.shist[kmin], heads);
-      } else if (head) {
-        atomicAdd(&S.shist[key], 1u);
-      }
-    }
-    if (active) {
-      hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
-      hp[HF_MASKS * N] = n.votes | n.keys << 16;
-      hp[HF_TERM * N] = n.term; hp[HF_COMMIT * N] = n.commit; hp[HF_LEN * N] = n.len;
-      hp[HF_DEADLINE * N] = n.deadline;
-      hp[HF_QMETA * N] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
-      hp[HF_REQ_ARR * N] = n.rq.arr; hp[HF_RES_ARR * N] = n.rs.arr;
-      hp[HF_REQ_TAIL * N] = n.rq.tail; hp[HF_RES_TAIL * N] = n.rs.tail;
-      hp[HF_ABASE * N] = n.base; hp[HF_AFRONT * N] = n.front; hp[HF_LED * N] = n.led;
-      hp[HF_TRACE_LO * N] = (uint32_t)n.trace; hp[HF_TRACE_HI * N] = (uint32_t)(n.trace >> 32);
-      if constexpr (nm_lds<N>()) {
-  #pragma unroll
-        for (int p = 0; p < N; ++p) {
-          hp[(HF_NEXT + p) * N] = nmL[p * 64 + lane];
-          hp[(HF_NEXT + N + p) * N] = nmL[(N + p) * 64 + lane];
-        }
-      }
-      if (k0 == 0) {
-        hc[0] = hidx; hc[1] = hterm; hc[2] = hval; hc[3] = cnext; hc[4] = ccount;
-      }
-    }
-  } while (CATCH && (wave += gridDim.x) * CPW < nslots);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  unsigned long long* const ctr = S.ctr + (size_t)(blockIdx.x % CTR_COPIES) * CTR_STRIDE;
-  if (lane < RAFT_CTR_COUNT) {
-    const uint32_t v = lctr[lane];
-    if (v) atomicAdd(&ctr[lane], (unsigned long long)v);
-  } else if (lane == LCTR_FIRSTVIOL) {
-    const uint32_t v = lctr[lane];
-    if (v != INF) atomicMin(&ctr[RAFT_CTR_COUNT], (unsigned long long)v);
-  } else if (lane == LCTR_PAYLOADMAX) {
-    const uint32_t v = lctr[lane];
-    if (v) atomicMax(&ctr[RAFT_CTR_COUNT + 1], (unsigned long long)v);
-  }
+  tick_wave<N, TRACE, SPEC, LITE>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x, gridDim.x, S.perm,
+                                  S.perm ? *S.nslots : S.C, nullptr, blockIdx.x);
 }
 
 // RAFT_SCHED_ALIGNED wave packing: a counting sort of the clusters by their next event tick
@@ -1501,10 +64,7 @@ static_assert(SCHED_CHUNKS == SCHED_PLAN_CHUNKS, "grid bound covers one partial 
 // Workgroups of the schedule kernel, each owning SCHED_KB buckets. Measured per rebuild (C2 65,536
 // / C3 1M clusters): 16 blocks 27.4 us / -, 64: 14.5 / 443 us, 256: 11.3 / 402 us, 512: 16.6 /
 // 322 us, 1024: 28.5 / 337 us (every block reads all keys; fewer buckets per block place faster).
-#ifndef RS_SCHED_BLOCKS
-#define RS_SCHED_BLOCKS 256
-#endif
-constexpr uint32_t SCHED_RANGE_BLOCKS = RS_SCHED_BLOCKS;
+constexpr uint32_t SCHED_RANGE_BLOCKS = 256;
 constexpr uint32_t SCHED_KB = SCHED_BUCKETS / SCHED_RANGE_BLOCKS;  // 64 buckets per block
 constexpr uint32_t SCHED_WINDOW = 0;
 static_assert(SCHED_CHUNKS == 1024 && SCHED_KB % SCHED_CHUNK == 0, "one chunk per thread");
@@ -1743,19 +303,10 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
   out[ci] = h;
 }
 
-#ifndef RS_KERNEL_ONLY   // scripts/quick_vgpr.sh compiles one instantiation without the launchers
 // The tick kernel's own start/stop timestamps go into ev0/ev1 through its dispatch packet
 // (hipExtLaunchKernelGGL): no marker packets between launches (each cost ~5.7 us of idle GPU).
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
-                         hipEvent_t ev0);
-
-// Catch-up waves: each takes wave slots in turn (tick_kernel<..., CATCH>). Few, so that an empty
-// catch-up launch costs little (the host falls back to the general kernel while many clusters
-// bail: raftsim.hip, steady_mode).
-#ifndef RS_CATCH_WAVES
-#define RS_CATCH_WAVES 256
-#endif
-constexpr uint32_t CATCH_WAVES = RS_CATCH_WAVES;
+                         hipEvent_t ev0, hipEvent_t ev1);
 
 template <int N, bool SPEC>
 hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
@@ -1764,20 +315,8 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = S.perm ? sched_slots_bound(S.C, N) / CPW : (S.C + CPW - 1) / CPW;
   if constexpr (N <= 5 && !SPEC) {
-    if (steady) {
-      // steady kernel over every cluster, then the general kernel over the clusters it bailed,
-      // each from the tick it stopped before; the launch's timing spans both
-      const hipError_t e = launch_steady(S, t0, nt, st, ev0);
-      if (e != hipSuccess) return e;
-      DevSim B = S;
-      B.perm = S.bail_c;
-      B.nslots = S.nbail;
-      B.resume = S.bail_t;
-      const uint32_t cw = std::min<uint32_t>((S.C + CPW - 1) / CPW, CATCH_WAVES);
-      hipExtLaunchKernelGGL((tick_kernel<N, false, false, true, true>), dim3(cw), dim3(64), lds, st,
-                            nullptr, ev1, 0, B, t0, nt);
-      return hipGetLastError();
-    }
+    // the steady kernel, whose workgroups run the clusters they bail through tick_wave
+    if (steady) return launch_steady(S, t0, nt, st, ev0, ev1);
   }
   if (S.TC)
     hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC, false>), dim3(waves), dim3(64), lds, st, ev0,
@@ -1798,8 +337,8 @@ hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
   return launch_tick_ns<N, false>(S, t0, nt, st, ev0, ev1, steady);
 }
 
-// steady: a LITE launch at N <= 5 without TRACE runs the steady kernel + catch-up (the caller
-// decides; results are the same either way)
+// steady: a LITE launch at N <= 5 without TRACE runs the steady kernel (the caller decides;
+// results are the same either way)
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
                        hipEvent_t ev1, bool steady) {
   switch (S.N) {
@@ -1829,12 +368,6 @@ hipError_t configure_n() {
       (e = configure_one<N, false, true>()) || (e = configure_one<N, true, true>()) ||
       (e = configure_one<N, false, false, true>()))
     return e;
-  if constexpr (N <= 5) {
-    if ((e = hipFuncSetAttribute(
-             reinterpret_cast<const void*>(tick_kernel<N, false, false, true, true>),
-             hipFuncAttributeMaxDynamicSharedMemorySize, (int)block_lds_bytes<N, false>())))
-      return e;
-  }
   return hipSuccess;
 }
 
@@ -1849,7 +382,6 @@ hipError_t configure_kernels() {
   return hipSuccess;
 }
 
-#endif  // RS_KERNEL_ONLY
 
 hipError_t launch_init(const DevSim& S, hipStream_t st) {
   hipLaunchKernelGGL(init_kernel, dim3((S.NN + 255) / 256), dim3(256), 0, st, S);

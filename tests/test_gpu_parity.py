@@ -135,11 +135,83 @@ def test_gpu_matches_oracle(name):
 
 @pytest.mark.parametrize("seed", [1, 42, 0xDEADBEEF, 0x1_2345_6789])
 def test_gpu_c2_full_size(seed):
-    """BASELINE config 2: 65,536 five-node clusters x 10k ticks, no faults, digest-equal, for the
-    seeds of SURVEY §8(d) and one above 2^32 (Philox key word 1 nonzero)."""
+    """BASELINE config 2: 65,536 five-node clusters, no faults, for the seeds of SURVEY §8(d) and
+    one above 2^32 (Philox key word 1 nonzero): digest-equal after each of four 10k-tick launches.
+    The first launch (elections) runs the general kernel; the last one is the steady kernel alone
+    on the 256-workgroup grid with no cluster bailed (core.clj:105-123,141-149,162-164)."""
     cfg = dict(n_clusters=65536, nodes=5, seed=seed)
-    g, r = run_pair(cfg, 10000, 10000)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    bails = []
+    for launch in range(4):
+        g.step(10000)
+        r.step(10000)
+        bails.append(g.diag_last_bails())
+        bad = np.nonzero(g.digest() != r.digest())[0]
+        assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
     assert g.counters() == r.counters()
+    assert bails[0] == -1 and bails[-1] == 0, bails
+
+
+@pytest.mark.parametrize("pack", ["dense", "identity"])
+def test_gpu_c2_bench_window(pack, monkeypatch):
+    """The exact window bench.py times for C2: seed 42, 65,536 clusters, 2 warm-up then 20 timed
+    10k-tick steps enqueued back to back (step_async + one sync), as the bench runs them;
+    digest-equal to the oracle after the warm-up and at the end, every counter equal."""
+    monkeypatch.setenv("RAFTSIM_STEADY_PACK", pack)
+    cfg = dict(n_clusters=65536, nodes=5, seed=42)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    for _ in range(2):
+        g.step(10000)
+        r.step(10000)
+    assert np.array_equal(g.digest(), r.digest())
+    for _ in range(20):
+        g.step_async(10000)
+    g.sync()
+    r.step(200000)
+    assert g.diag_last_bails() == 0
+    assert np.array_equal(g.digest(), r.digest())
+    assert g.counters() == r.counters()
+
+
+def _client_set_into(be, cluster, node, value):
+    """Append a client-set (SIM_SPEC §3, server.clj:12) to a node's REQ queue, arriving now."""
+    q = [list(m) for m in be.read_queue(cluster, node, 0)]
+    arr = max([be.tick] + [m[0] for m in q])
+    be.write_queue(cluster, node, 0, q + [[arr, 3, 0, value, 0, 0, 0, 0]])
+
+
+@pytest.mark.parametrize("mode", ["auto", "always"])
+@pytest.mark.parametrize("event", ["set_tick", "client_set", "client_cursor"])
+def test_gpu_host_writes_after_lite_launches(event, mode, monkeypatch):
+    """Host writes after 14 LITE launches (past the 8-launch packing period, with the packing
+    reused between rebuilds): set_tick, a queued client-set and a finite client cursor (both clear
+    LITE for the rest of the handle) land at every phase of the rebuild cycle; GPU == oracle after
+    each of the next 10 launches (raftsim.hip: packing keys and histogram stay consistent)."""
+    monkeypatch.setenv("RAFTSIM_STEADY", mode)
+    cfg = dict(n_clusters=4096, nodes=5, seed=42, ticks_per_launch=1000, log_cap=64)
+    for phase in (0, 3):
+        g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+        helpers.oracle_threads(r, helpers.cpu_threads())
+        for _ in range(14 + phase):
+            g.step(1000)
+            r.step(1000)
+        for be in (g, r):
+            if event == "set_tick":
+                be.set_tick(be.tick + 777)
+            elif event == "client_set":
+                for c in (5, 100, 4095):
+                    _client_set_into(be, c, 1 + c % 5, 1000 + c)
+            else:
+                be.write_clusters(7, [dict(hwm=(0, 0, 0), client_next=be.tick + 100,
+                                           client_count=0)])
+        for launch in range(10):
+            g.step(1000)
+            r.step(1000)
+            bad = np.nonzero(g.digest() != r.digest())[0]
+            assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
+        assert g.counters() == r.counters()
 
 
 @pytest.mark.parametrize("nodes", [7, 9])
@@ -377,12 +449,15 @@ LITE_CASES = ["c2_small", "lite_n2", "lite_n3", "lite_n4", "lite_elections", "li
               "lite_odd_launches", "lite_short_round"]
 
 
+@pytest.mark.parametrize("pack", ["dense", "identity"])
 @pytest.mark.parametrize("name", LITE_CASES)
-def test_gpu_forced_steady_matches_oracle(name, monkeypatch):
+def test_gpu_forced_steady_matches_oracle(name, pack, monkeypatch):
     """Every LITE launch on the steady kernel (RAFTSIM_STEADY=always), from init-node: elections
-    and every other event outside its model go through the catch-up launch, whose waves take
-    several wave slots each; GPU == oracle after every chunk."""
+    and every other event outside its model go through the workgroup's catch-up (the general
+    tick body over the clusters it bailed, several wave slots per wave); GPU == oracle after
+    every chunk."""
     monkeypatch.setenv("RAFTSIM_STEADY", "always")
+    monkeypatch.setenv("RAFTSIM_STEADY_PACK", pack)
     cfg = CASES[name]
     g, r = run_pair(cfg, 20000, 5000)
     assert g.counters() == r.counters()
