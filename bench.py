@@ -7,28 +7,40 @@ simulates its own 65,536 clusters (global ids rank*65536 + i: disjoint, shard-in
 streams; weak scaling, no data-path collective). C2 is periodic in steady state (heartbeat rounds
 every hb ticks), so its window is the K steps after W warm-up steps.
 
-The same JSON line carries, under "workloads", BASELINE config 3 ("C3"): 1,048,576 five-node
-clusters with 10 % drop, 1 % duplication, delay U[1,50], partitions and a bursty client that
-follows redirects (SIM_SPEC D14/D15; one client-set per 100 ticks on average), and the same traffic
-under the Spec-Raft control ("C3-spec", SIM_SPEC §8: no crash storm, real replication at 1M
-clusters). Under the faithful handlers C3 turns into a crash storm whose cost per tick changes as
-nodes halt, so the C3 windows are fixed: ticks [0, 10,000 K) from init-node on a fresh handle (the
-W warm-up steps run on a throwaway handle of the same shape), and the line reports the live-node
-fraction at the window's end and the live node-ticks/s. Under torchrun the 1M clusters are split
-across the ranks (strong scaling).
+Timing. Each rank enqueues its K steps on the simulator's stream and syncs once; the device time
+of the K steps is taken from HIP events on that stream (raft_sim_last_span: from before the first
+launch to after the last), MAX-reduced over ranks, and `value` = all ranks' node-ticks / that
+time. The K steps are also bracketed by a barrier + torch.cuda.synchronize() on both sides and the
+wall time around them is reported as `wall_ms_per_step` (it adds the host's sync and, under
+torchrun, barrier latency, which at C2's ~0.03 ms per step would dominate a 20-step span).
+
+The same JSON line carries, under "workloads", the other BASELINE configs:
+  c2_init   config 2 as named: ticks [0, 10,000) from init-node (every cluster elects its first
+            leader), on `reps` fresh handles.
+  c3        config 3: 1,048,576 five-node clusters with 10 % drop, 1 % duplication, delay U[1,50],
+            partitions and a bursty client that follows redirects (SIM_SPEC D14/D15; one
+            client-set per 100 ticks on average), ticks [0, 10,000 K) from init-node on a fresh
+            handle (the W warm-up steps run on a throwaway handle); under the faithful handlers a
+            crash storm, so the line reports the live-node fraction at the window's end.
+  c3_spec   the same traffic under the Spec-Raft control (SIM_SPEC §8): real replication at 1M.
+  c4_n9     config 4: 16,384 nine-node clusters per GPU, 4096-entry logs, bursty client
+            (1000+-entry AppendEntries batches, OVERFLOW halts), K steps after W warm-up steps.
+  c5        config 5: config 3's faults and client with the vote granted without the up-to-date
+            check on the Spec-Raft protocol (variant flags 3), 131,072 clusters per GPU, stepped
+            1,000 ticks at a time until a safety violation is counted anywhere in the job (a MIN
+            all-reduce of the first-violation tick over RCCL per chunk); time to it, and the C
+            oracle's time to the same tick on the same clusters.
 
 Per workload:
-  roofline      the tick kernel against HBM bandwidth with the event model of DESIGN.md: per launch
-                the hot node state in and out once (2 * S_node(N) bytes per node, S_node = 32 + 8N),
-                64 B per delivered message (written and read once) and 16 B per appended log entry
-                (read and written once), over the average launch time measured with HIP events on
-                the simulator's stream. `traffic` is the PMC-measured HBM bytes per launch from
-                pmc_traffic.json (scripts/summarize_profile.py), used only when it was measured on
-                this kernel build (source hash) over this same window (steps, warm-up, window kind).
-                `bound` is the roofline axis (HBM); the measured limiter is named in `limiter`.
-                `frac_state_model` prices only the hot state in and out: a C2 launch on the
-                lane-per-cluster steady kernel keeps its messages in registers, so the event
-                model's 64 B per message is not HBM traffic there (PMC `traffic` shows it).
+  roofline      the tick kernel against HBM bandwidth. `achieved` = the compulsory bytes of a
+                launch -- the hot node state in and out once, 2 * S_node(N) bytes per node
+                (S_node = 32 + 8N) -- over the average launch time measured with HIP
+                events on the simulator's stream; `frac` = achieved / 8 TB/s. `traffic` = the
+                PMC-measured HBM bytes per launch (pmc_traffic.json, scripts/summarize_profile.py),
+                used only when measured on this kernel build (source hash) over this window.
+                `frac_event_model` prices SURVEY's event model instead (+ 64 B per delivered
+                message + 16 B per appended entry); the steady kernel keeps C2's messages in
+                registers, so those bytes never reach HBM there.
   cpu_baseline  the C oracle (oracle/raftref.c, the restatement of core.clj/log.clj; "port") on a
                 bounded sample of the same workload over the same tick window, clusters mapped over
                 every host CPU this process may run on (the pmap analogue), with the same
@@ -65,36 +77,42 @@ WORKLOADS = {
                cpu=(65536, 40),
                desc="C2: 65,536 five-node clusters per GPU x 10,000 ticks per step, no faults, "
                     "no client"),
+    "c2_init": dict(cfg=dict(nodes=5, seed=42), clusters=65536, scaling="weak", window="first",
+                    cpu=65536, reps=5,
+                    desc="C2 as named: 65,536 five-node clusters per GPU, ticks [0, 10,000) from "
+                         "init-node (first elections included), no faults, no client"),
     "c3": dict(cfg=C3_CFG, clusters=1 << 20, scaling="strong", window="init", cpu=1 << 19,
                desc="C3: " + C3_DESC),
     "c3_spec": dict(cfg=dict(C3_CFG, variant_flags=2, log_cap=1024), clusters=1 << 20,
                     scaling="strong", window="init", cpu=1 << 19,
                     desc="C3 under the Spec-Raft control (SIM_SPEC §8, 1024-entry logs): "
                          + C3_DESC),
-    "c4_n7": dict(cfg=dict(nodes=7, seed=3, log_cap=4096, client_ppm=500000, client_period=8192,
-                           client_burst=2048, client_redirects=4),
-                  clusters=16384, scaling="weak", window="steady", cpu=(16384, 2),
-                  desc="C4: 16,384 seven-node clusters, 4096-entry logs, bursty client "
-                       "(1000+-entry batches)"),
     "c4_n9": dict(cfg=dict(nodes=9, seed=5, log_cap=4096, client_ppm=500000, client_period=8192,
                            client_burst=2048, client_redirects=4),
-                  clusters=16384, scaling="weak", window="steady", cpu=(16384, 2),
-                  desc="C4: 16,384 nine-node clusters, 4096-entry logs, bursty client "
-                       "(1000+-entry batches)"),
+                  clusters=16384, scaling="weak", window="steady", cpu=(8192, 2),
+                  desc="C4: 16,384 nine-node clusters per GPU, 4096-entry logs, bursty client "
+                       "(500,000 ppm in 2048 of every 8192 ticks, redirects followed: 1000+-entry "
+                       "AppendEntries batches, OVERFLOW halts)"),
+    "c5": dict(cfg=dict(C3_CFG, variant_flags=3, log_cap=1024), clusters=131072, scaling="weak",
+               window="violation", chunk=1000, max_ticks=200000,
+               desc="C5: 131,072 five-node clusters per GPU with C3's faults and client, Spec-Raft "
+                    "with the vote granted without the up-to-date check (variant flags 3); "
+                    "stepped 1,000 ticks at a time from init-node until a safety violation is "
+                    "counted anywhere in the job"),
 }
-KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip", "raft-simulation_amd/csrc/steady_kernel.hip",
-                  "raft-simulation_amd/csrc/device.hpp",
+KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip",
+                  "raft-simulation_amd/csrc/steady_kernel.hip",
+                  "raft-simulation_amd/csrc/tick_wave.hpp", "raft-simulation_amd/csrc/device.hpp",
                   "raft-simulation_amd/csrc/raftsim.hip", "include/raftsim.h"]
 HALTS = ("halt_ioobe", "halt_npe", "halt_cce", "halt_overflow")
 LIMITER = {
-    "c2": "one wave per SIMD running 64 clusters' heartbeat rounds: the chain of dependent "
-          "quarter-rate multiplies (Philox draws, FNV trace hash) per trip, then the state load "
-          "and the write-back's per-lane L2 requests (per-wave timeline, DESIGN.md); messages stay "
-          "in registers, so the event model's message bytes are not HBM traffic (see "
-          "frac_state_model and traffic)",
-    "c3": "issue of the active trips' divergent instruction stream (client-set injections and "
-          "redirect hops, most of them into halted nodes; PMC instruction counts, DESIGN.md), not "
-          "HBM bandwidth",
+    "steady": "one wave per SIMD running 64 clusters' heartbeat rounds (C2 has exactly 64 clusters "
+              "per SIMD): the state load, the chain of dependent multiplies per trip (trace hash; "
+              "one Philox draw per follower per launch) and the write-back, in sequence "
+              "(per-wave timeline, DESIGN.md); messages stay in registers",
+    "general": "issue of the active trips' divergent instruction stream (client-set injections, "
+               "redirect hops, replication and checker trips; PMC instruction counts, DESIGN.md), "
+               "not HBM bandwidth",
 }
 
 
@@ -107,9 +125,14 @@ def kernel_build_hash():
 
 def window_id(spec, args):
     """The tick window a number describes: steady windows are the K steps after W warm-up steps
-    (periodic state: any K), init windows ticks [0, 10000 K) from init-node."""
+    (periodic state: any K), init windows ticks [0, 10000 K) from init-node, first windows ticks
+    [0, 10000) from init-node, violation windows from init-node to the first violation."""
     if spec["window"] == "init":
         return {"kind": "init", "steps": args.steps}
+    if spec["window"] == "first":
+        return {"kind": "first", "steps": 1}
+    if spec["window"] == "violation":
+        return {"kind": "violation", "chunk": spec["chunk"]}
     return {"kind": "steady", "steps": args.steps, "warmup": args.warmup}
 
 
@@ -125,7 +148,7 @@ def load_traffic(workload, window):
         return None, f"no PMC profile of {workload}"
     if rec.get("kernel_src_sha") != kernel_build_hash():
         return None, "PMC profile of another kernel build"
-    if window["kind"] == "init" and rec.get("window") != window:
+    if rec.get("window") != window:
         return None, f"PMC profile window {rec.get('window')} is not this window"
     return rec.get("hbm_bytes_per_launch"), rec.get("source")
 
@@ -155,6 +178,8 @@ def cpu_baseline(spec, args):
     if spec["window"] == "init":
         steps = args.steps
         clusters = max(1024, min(spec["clusters"], spec["cpu"] // max(1, steps)))
+    elif spec["window"] == "first":
+        clusters, steps = spec["cpu"], 1
     else:
         clusters, steps = spec["cpu"]
 
@@ -173,8 +198,8 @@ def cpu_baseline(spec, args):
     warm = spec["window"] == "steady"
     v, dt = rate(clusters, steps, True, warm)
     v_every, dt_every = rate(max(1, clusters // 8), 1, False, warm)
-    where = (f"ticks [0, {steps * TICKS_PER_STEP}) from init-node (the GPU's window)"
-             if not warm else f"{steps} steps after a warm-up step")
+    where = (f"{steps} steps after a warm-up step" if warm
+             else f"ticks [0, {steps * TICKS_PER_STEP}) from init-node (the GPU's window)")
     return {"value": v, "unit": "node-ticks/s", "cores": threads, "kind": "port",
             "sample": f"{clusters} clusters x {cfg['nodes']} nodes, {where}, oracle/raftref.c "
                       f"with the same idle-tick skipping as the kernel, {threads} threads (the host "
@@ -184,6 +209,31 @@ def cpu_baseline(spec, args):
             "every_tick_value": v_every,
             "every_tick_sample": f"{max(1, clusters // 8)} clusters x 1 step visiting every tick, "
                                  f"{dt_every:.2f} s"}
+
+
+def roofline(name, spec, count, n, launches, avg_launch_ms, delta, window, world):
+    """Compulsory-byte roofline of the dominant kernel (per launch of one rank's shard)."""
+    total_launches = max(1, launches * world)
+    s_node = 32 + 8 * n
+    msgs = delta["delivered"] / total_launches
+    entries = delta["entries_appended"] / total_launches
+    state_bytes = 2 * s_node * count * n
+    event_bytes = state_bytes + 64 * msgs + 16 * entries
+    gbs = (lambda b: b / (avg_launch_ms * 1e-3) / 1e9) if avg_launch_ms else (lambda b: 0.0)
+    traffic, traffic_src = load_traffic(name, window)
+    steady = spec["cfg"]["nodes"] <= 5 and not spec["cfg"].get("client_ppm") and \
+        spec["window"] in ("steady",)
+    return {"bound": "hbm", "achieved": gbs(state_bytes), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs(state_bytes) / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": traffic_src,
+            "model": "compulsory: the hot node state in and out once, 2 * S_node * nodes per "
+                     "launch (S_node = 32 + 8N bytes)",
+            "bytes_per_launch": state_bytes, "avg_launch_ms": avg_launch_ms,
+            "traffic_over_compulsory": traffic / state_bytes if traffic else None,
+            "frac_event_model": gbs(event_bytes) / HBM_PEAK_GBS,
+            "event_bytes_per_launch": event_bytes,
+            "launches": launches, "kernel_src_sha": kernel_build_hash(),
+            "limiter": LIMITER["steady" if steady else "general"]}
 
 
 def run_workload(name, args, world, rank, local_rank, dist):
@@ -201,42 +251,66 @@ def run_workload(name, args, world, rank, local_rank, dist):
     else:
         offset, count = rdist.shard(clusters, rank, world)
         total = clusters
+    dev = f"cuda:{local_rank}"
 
     def make():
         return raftsim.Simulator(n_clusters=count, cluster_offset=offset, device=local_rank, **cfg)
 
-    def sync():
+    def barrier():
         if dist is not None:
             import torch
 
             torch.cuda.synchronize()
             dist.barrier()
 
-    init = spec["window"] == "init"
-    if init:
-        if args.warmup:                    # same shape, thrown away: the window starts at init
-            w = make()
-            for _ in range(args.warmup):
-                w.step(TICKS_PER_STEP)
-            w.sync()
-            w.close()
-        sim = make()
-    else:
-        sim = make()
+    window = window_id(spec, args)
+    kind = spec["window"]
+    extra = {}
+    if kind == "violation":
+        return run_violation(name, spec, args, world, rank, dist, make, count, total, offset)
+    if kind == "init" and args.warmup:       # same shape, thrown away: the window starts at init
+        w = make()
+        for _ in range(args.warmup):
+            w.step(TICKS_PER_STEP)
+        w.sync()
+        w.close()
+    sims = [make()] if kind != "first" else []
+    sim = sims[0] if sims else None
+    if kind == "steady":
         for _ in range(args.warmup):
             sim.step(TICKS_PER_STEP)
-    c_before = sim.counters()
     nodes = count * n
-    live = [nodes - sum(c_before[h] for h in HALTS)]
-    sync()
+    c_before = sim.counters() if sim else None
+    live = [nodes - sum(c_before[h] for h in HALTS)] if sim else []
+    steps = args.steps if kind != "first" else 1
+    barrier()
     t0 = time.perf_counter()
-    kernel_ms, launches = 0.0, 0
-    if init:
+    span_ms, kernel_ms, launches = 0.0, 0.0, 0
+    if kind == "first":
+        # config 2 as named: a fresh handle per repetition, one 10k-tick step from init-node
+        reps = spec["reps"]
+        c_sum = None
+        for _ in range(reps):
+            s = make()
+            s.step_async(TICKS_PER_STEP)
+            s.sync()
+            span_ms += s.last_span()
+            ms, nl = s.last_step_timing()
+            kernel_ms += ms * nl
+            launches += nl
+            c = s.counters()
+            c_sum = c if c_sum is None else {k: (c_sum[k] + c[k]) if isinstance(c[k], int) and
+                                             k not in ("first_violation_tick", "payload_max")
+                                             else c[k] for k in c}
+            s.close()
+        steps = reps
+    elif kind == "init":
         # one sync per step: the live-node count after every step (halts are permanent, so the
-        # halt counters count the halted nodes) for the live node-ticks of the window
-        for _ in range(args.steps):
+        # halt counters count the halted nodes); the device time of each step is its own span
+        for _ in range(steps):
             sim.step_async(TICKS_PER_STEP)
             sim.sync()
+            span_ms += sim.last_span()
             ms, nl = sim.last_step_timing()
             kernel_ms += ms * nl
             launches += nl
@@ -244,28 +318,33 @@ def run_workload(name, args, world, rank, local_rank, dist):
             live.append(nodes - sum(c[h] for h in HALTS))
     else:
         # K steps enqueued back to back on the simulator's stream (raft_sim_step_async), then one
-        # raft_sim_sync: per-launch HIP events still time every tick-kernel launch of the K steps
-        for _ in range(args.steps):
+        # raft_sim_sync: HIP events time the whole span and every tick-kernel launch in it
+        for _ in range(steps):
             sim.step_async(TICKS_PER_STEP)
         sim.sync()
+        span_ms = sim.last_span()
         ms, launches = sim.last_step_timing()
         kernel_ms = ms * launches
-    sync()
-    elapsed = time.perf_counter() - t0
+    barrier()
+    wall = time.perf_counter() - t0
     avg_launch_ms = kernel_ms / max(1, launches)
-    c_after = sim.counters()
-    if not init:
-        live.append(nodes - sum(c_after[h] for h in HALTS))
-    delta = {k: c_after[k] - c_before[k] for k in c_after
-             if k not in ("first_violation_tick", "payload_max")}
-    delta["payload_max"] = c_after["payload_max"]
-    delta["first_violation_tick"] = c_after["first_violation_tick"]
-    live_ticks = sum((a + b) / 2 for a, b in zip(live, live[1:])) * TICKS_PER_STEP \
-        if init else (live[0] + live[-1]) / 2 * TICKS_PER_STEP * args.steps
-    elapsed_max = elapsed
+    if kind == "first":
+        delta = {k: v for k, v in c_sum.items()}
+        live = [nodes, nodes - sum(c_sum[h] for h in HALTS) // max(1, spec["reps"])]
+    else:
+        c_after = sim.counters()
+        if kind == "steady":
+            live.append(nodes - sum(c_after[h] for h in HALTS))
+        delta = {k: c_after[k] - c_before[k] for k in c_after
+                 if k not in ("first_violation_tick", "payload_max")}
+        delta["payload_max"] = c_after["payload_max"]
+        delta["first_violation_tick"] = c_after["first_violation_tick"]
+    live_ticks = (sum((a + b) / 2 for a, b in zip(live, live[1:])) * TICKS_PER_STEP
+                  if kind == "init" else (live[0] + live[-1]) / 2 * TICKS_PER_STEP * steps)
+    span_max, wall_max = span_ms, wall
     if dist is not None:
-        dev = f"cuda:{local_rank}"
-        elapsed_max = rdist.reduce_max(elapsed, dev)
+        span_max = rdist.reduce_max(span_ms, dev)
+        wall_max = rdist.reduce_max(wall, dev)
         delta = rdist.reduce_counters(delta, dev)
         avg_launch_ms = rdist.reduce_max(avg_launch_ms, dev)
         live_ticks = rdist.reduce_sum(live_ticks, dev)
@@ -273,55 +352,95 @@ def run_workload(name, args, world, rank, local_rank, dist):
     else:
         live_end = float(live[-1])
     node_ticks = delta["node_ticks"]
-
-    # event model (per launch of one rank's shard): hot state in + out, 64 B per delivered
-    # message, 16 B per appended entry (counts are whole-job, divided back to one launch)
-    total_launches = max(1, launches * world)
-    s_node = 32 + 8 * n
-    msgs = delta["delivered"] / total_launches
-    entries = delta["entries_appended"] / total_launches
-    state_bytes = 2 * s_node * count * n
-    event_bytes = state_bytes + 64 * msgs + 16 * entries
-    achieved = event_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms else 0.0
-    ticks_per_launch = args.steps * TICKS_PER_STEP / max(1, launches)
-    window = window_id(spec, args)
-    traffic, traffic_src = load_traffic(name, window)
     rec = {
-        "value": node_ticks / elapsed_max,
+        "value": node_ticks / (span_max * 1e-3),
         "unit": "node-ticks/s",
-        "ms_per_step": elapsed_max * 1e3 / args.steps,
+        "ms_per_step": span_max / steps,
+        "wall_ms_per_step": wall_max * 1e3 / steps,
+        "wall_value": node_ticks / wall_max,
+        "timing": "device time of the steps (HIP events on the simulator's stream, MAX over "
+                  "ranks); wall_* = perf_counter around them, barrier + synchronize both sides",
         "scaling": scaling,
         "window": window,
         "config": {"workload": spec["desc"], "clusters": total, "clusters_per_gpu": count,
                    "nodes": n, "ticks_per_step": TICKS_PER_STEP,
                    "parallelism": f"cluster-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "model": "event: 2*S_node*nodes + 64 B/delivered msg + 16 B/appended entry "
-                              "per launch",
-                     "bytes_per_launch": event_bytes, "avg_launch_ms": avg_launch_ms,
-                     # the hot node state in and out once: what a launch that keeps its messages
-                     # on chip (the lane-per-cluster steady kernel) must move through HBM
-                     "state_bytes_per_launch": state_bytes,
-                     "frac_state_model": state_bytes / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                     if avg_launch_ms else 0.0,
-                     "launches": launches, "ticks_per_launch": ticks_per_launch,
-                     "kernel_src_sha": kernel_build_hash(),
-                     "limiter": LIMITER["c2" if name == "c2" else "c3"]},
+        "roofline": roofline(name, spec, count, n, launches, avg_launch_ms, delta, window, world),
+        "events_per_s": sum(delta[k] for k in delta if k.startswith("ev_")) / (span_max * 1e-3),
         "live_node_frac_end": live_end / (total * n),
-        "live_node_ticks_per_s": live_ticks / elapsed_max if dist is None
-        else live_ticks / elapsed_max,
+        "live_node_ticks_per_s": live_ticks / (span_max * 1e-3),
         "payload_evicted": delta["payload_evicted"],
         "counters": {k: v for k, v in delta.items() if v},
-        "sched_note": "C3 windows sync once per step to count live nodes (counter read ~0.05 ms "
-                      "per step, inside the timed region)" if init else None,
+        **extra,
     }
+    if kind == "first":
+        rec["reps"] = spec["reps"]
     if delta["payload_evicted"]:
         # SIM_SPEC §4 P3: an evicted payload entry is the simulator's one fidelity limit
         rec["fidelity_warning"] = "payload entries were evicted from a sender's arena"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(spec, args)
+    for s in sims:
+        s.close()
+    return rec
+
+
+def run_violation(name, spec, args, world, rank, dist, make, count, total, offset):
+    """BASELINE config 5: step every rank's clusters chunk by chunk until a violation is counted
+    anywhere in the job (MIN all-reduce of the first-violation tick per chunk over RCCL)."""
+    from raftsim import dist as rdist
+
+    cfg, n = spec["cfg"], spec["cfg"]["nodes"]
+    dev = f"cuda:{os.environ.get('LOCAL_RANK', '0')}"
+    red = (lambda x: rdist.reduce_min(x, dev)) if dist is not None else None
+    sim = make()
+    t0 = time.perf_counter()
+    fv, ticks, (span_ms, kms, launches) = rdist.first_violation_search(
+        sim, spec["chunk"], spec["max_ticks"], red)
+    wall = time.perf_counter() - t0
+    avg_launch_ms = kms / max(1, launches)
+    c = sim.counters()
+    span_max = span_ms
+    if dist is not None:
+        span_max = rdist.reduce_max(span_ms, dev)
+        avg_launch_ms = rdist.reduce_max(avg_launch_ms, dev)
+        c = rdist.reduce_counters(c, dev)
+    window = window_id(spec, args)
+    rec = {
+        "value": c["node_ticks"] / (span_max * 1e-3),
+        "unit": "node-ticks/s",
+        "first_violation_tick": fv,
+        "ticks_simulated": ticks,
+        "time_to_first_violation_s": span_max * 1e-3,
+        "wall_s": wall,
+        "timing": "device time of the chunks (HIP events, MAX over ranks); wall_s adds the "
+                  "per-chunk counter reads and all-reduces",
+        "scaling": "weak",
+        "window": window,
+        "config": {"workload": spec["desc"], "clusters": total, "clusters_per_gpu": count,
+                   "nodes": n, "ticks_per_chunk": spec["chunk"],
+                   "parallelism": f"cluster-sharded x{world}"},
+        "roofline": roofline(name, spec, count, n, launches, avg_launch_ms, c, window, world),
+        "counters": {k: v for k, v in c.items() if v},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import helpers
+
+        ref = helpers.oracle(n_clusters=count, cluster_offset=offset, **cfg)
+        threads = helpers.cpu_threads()
+        helpers.oracle_threads(ref, threads)
+        helpers.oracle_idle_skip(ref, True)
+        t1 = time.perf_counter()
+        cfv, cticks, _ = rdist.first_violation_search(ref, spec["chunk"], ticks)
+        dt = time.perf_counter() - t1
+        rec["cpu_baseline"] = {
+            "value": count * n * cticks / dt, "unit": "node-ticks/s", "cores": threads,
+            "kind": "port", "time_to_first_violation_s": dt, "first_violation_tick": cfv,
+            "bit_exact": cfv == fv and cticks == ticks and bool((sim.digest() == ref.digest()).all()),
+            "sample": f"the same {count} clusters x {n} nodes from init-node in the same "
+                      f"{spec['chunk']}-tick chunks, oracle/raftref.c with idle-tick skipping, "
+                      f"{threads} threads, {dt:.2f} s",
+            "host_cpus": host_cpus()}
     sim.close()
     return rec
 
@@ -331,7 +450,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2+c3+c3_spec",
+    ap.add_argument("--workload", default="c2+c2_init+c3+c3_spec+c4_n9+c5",
                     help="headline[+extra...] from " + ", ".join(WORKLOADS))
     ap.add_argument("--clusters", type=int, default=0, help="override the headline's clusters")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -368,12 +487,11 @@ def main():
             "data": "synthetic (seeded Philox clusters from init-node state)",
             "config": head["config"],
             "roofline": head["roofline"],
-            "window": head["window"],
-            "payload_evicted": head["payload_evicted"],
-            "counters": head["counters"],
         }
-        if "cpu_baseline" in head:
-            out["cpu_baseline"] = head["cpu_baseline"]
+        for k in ("wall_ms_per_step", "wall_value", "timing", "window", "events_per_s",
+                  "payload_evicted", "counters", "cpu_baseline"):
+            if k in head:
+                out[k] = head[k]
         if len(names) > 1:
             out["workloads"] = {name: recs[name] for name in names[1:]}
         print(json.dumps(out), flush=True)

@@ -246,6 +246,12 @@ int raft_sim_digest(raft_sim_t* sim, uint32_t c0, uint32_t nc, uint64_t* out);
  * between launches are excluded -- and their count; for bench.py's roofline. */
 int raft_sim_last_step_timing(raft_sim_t* sim, double* avg_kernel_ms, uint32_t* launches);
 
+/* Device time of everything the last raft_sim_step (or every raft_sim_step_async since the
+ * previous sync, once raft_sim_sync returned) enqueued, from a HIP event before its first launch
+ * to one after its last, on each shard's stream; the maximum over shards. Host time spent between
+ * steps is not in it; gaps between the queued launches are. For bench.py's throughput. */
+int raft_sim_last_span(raft_sim_t* sim, double* span_ms);
+
 void raft_sim_destroy(raft_sim_t* sim);
 const char* raft_sim_last_error(void);
 

@@ -67,8 +67,6 @@ struct DevSim {
   uint32_t* wavelog;        // diagnostic builds (RS_WAVELOG) only: [waves][8] per-wave timeline
   uint32_t lite;            // no client traffic (and no finite client cursor), no faults, fixed
                             // delay: the LITE tick kernel applies
-  uint32_t perm_dense;      // the packing was planned without padding (one slot per cluster:
-                            // nslots == C), for the lane-per-cluster steady kernel
   // Steady kernel (steady_kernel.hip): clusters it stops ("bails") at a tick it does not model
   // are run from that tick by the same workgroup through the general tick body; their count is
   // summed here for the host's path choice (speed only).

@@ -14,7 +14,7 @@ hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st
                        hipEvent_t ev1, bool steady);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
-                             hipStream_t st, bool dense);
+                             hipStream_t st);
 hipError_t launch_init(const DevSim& S, hipStream_t st);
 hipError_t launch_digest(const DevSim& S, uint32_t c0, uint32_t nc, unsigned long long* out,
                          hipStream_t st);
@@ -67,7 +67,6 @@ struct Shard {
   // counters alternate between steady launches (each reports and zeroes the other)
   bool steady_ok;
   bool last_steady;                    // the last tick launch took the steady path
-  bool steady_identity;                // steady launches run the clusters in id order (no packing)
   uint32_t* nbail2;
   uint32_t steady_parity;
   // Path choice per launch (speed only: both paths give the same state). RAFTSIM_STEADY=auto
@@ -234,8 +233,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   if (s->steady_ok) {
     const char* m = getenv("RAFTSIM_STEADY");
     s->steady_mode = m && !strcmp(m, "always") ? 1 : m && !strcmp(m, "never") ? 2 : 0;
-    const char* pk = getenv("RAFTSIM_STEADY_PACK");
-    s->steady_identity = pk && !strcmp(pk, "identity");
+
     s->steady_cooldown = 1;
     void* hp = nullptr;
     if (hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
@@ -311,8 +309,10 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     }
     bool no_keys = false;                // this launch writes no packing keys
     bool no_perm = false;
-    if (steady && s->steady_identity) {
-      // clusters in id order: no packing, no keys
+    if (steady) {
+      // the steady kernel runs the clusters in id order: no packing, no keys. (Packed by next
+      // event, 64 to a wave, the same launch took 0.0329 against 0.0318 ms: a lane runs its own
+      // cluster's clock, and the packing's perm load sat in front of every state load.)
       no_perm = no_keys = true;
       s->keys_written = false;
     } else if (s->cfg.schedule == RAFT_SCHED_ALIGNED) {
@@ -325,12 +325,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
           HIP_OK(hipMemsetAsync(s->d.shist, 0, rs::SCHED_BUCKETS * 4, s->stream));
           HIP_OK(rs::launch_sched_key(s->d, t0, s->stream));
         }
-        // LITE launches on the steady path: one slot per cluster, no padding (the lane kernel
-        // takes 64 consecutive slots per wave); otherwise chunks of whole waves. lite never comes
-        // back once cleared, so a packing used by a steady launch is always dense.
-        const bool dense = s->steady_ok && s->d.lite;
-        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream, dense));
-        s->d.perm_dense = dense;
+        HIP_OK(rs::launch_sched_perm(s->d, s->soff, s->sperm, s->snslots, s->stream));
         // the schedule kernel read d.shist and zeroed soff: the next key-writing launch fills it
         std::swap(s->d.shist, s->soff);
         s->d.perm = s->sperm;
@@ -340,7 +335,6 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       s->keys_written = s->resort_ctr % s->resort_every == 0;   // the next launch rebuilds
       no_keys = !s->keys_written;
     }
-    if (steady && s->d.perm && !s->d.perm_dense) steady = false;   // (not reachable: see above)
     while (s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -875,6 +869,14 @@ int raft_sim_last_step_timing(raft_sim_t* r, double* avg_kernel_ms, uint32_t* la
   }
   *avg_kernel_ms = n ? sum / n : 0.0;
   *launches = r->sh.empty() ? 0 : r->sh[0]->last_launches;
+  return 0;
+}
+
+int raft_sim_last_span(raft_sim_t* r, double* span_ms) {
+  if (!r || !span_ms) return fail(-EINVAL, "null argument");
+  double m = 0;
+  for (Shard* s : r->sh) m = std::max(m, s->last_step_ms);
+  *span_ms = m;
   return 0;
 }
 

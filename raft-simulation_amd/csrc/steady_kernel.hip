@@ -65,7 +65,6 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   __shared__ uint32_t nbl;                         // clusters this workgroup bailed
   __shared__ uint32_t bl_c[LANE_WG], bl_t[LANE_WG];   // bailed cluster, tick it stopped before
   extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
-  const uint32_t nslots = S.perm ? *S.nslots : S.C;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // the previous steady launch's bail count (complete: that launch has ended) to the host, which
     // picks the next launches' path from it (speed only); that word is this launch's successor's
@@ -73,13 +72,12 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     if (S.bail_report) *S.bail_report = prev;
     *S.nbail_zero = 0;
   }
-  if (blockIdx.x * LANE_WG >= nslots) return;                  // workgroup-uniform
   if (threadIdx.x < 4) sctr[threadIdx.x] = 0;
   if (threadIdx.x == 0) nbl = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t slot = blockIdx.x * LANE_WG + threadIdx.x;
-  const uint32_t c0 = slot < nslots ? (S.perm ? S.perm[slot] : slot) : INF;
+  const uint32_t c0 = blockIdx.x * LANE_WG + threadIdx.x < S.C ? blockIdx.x * LANE_WG + threadIdx.x
+                                                                 : INF;   // clusters in id order
   const bool active = c0 != INF;
   const uint32_t c = active ? c0 : 0u;
   const uint32_t g = S.goff + c;
@@ -604,12 +602,11 @@ hipError_t configure_steady() {
   return e;
 }
 
-// The steady kernel for N <= 5 (LITE launches; the caller checks): one thread per packing slot,
-// which is one per cluster (dense packing or the identity). Its timestamps go into ev0/ev1 through
-// its dispatch packet.
+// The steady kernel for N <= 5 (LITE launches; the caller checks): one thread per cluster, in id
+// order. Its timestamps go into ev0/ev1 through its dispatch packet.
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0, hipEvent_t ev1) {
-  if (S.perm && !S.perm_dense) return hipErrorInvalidValue;   // padded slots: not this kernel's
+  if (S.perm) return hipErrorInvalidValue;                     // clusters in id order only
   const dim3 grid((S.C + LANE_WG - 1) / LANE_WG);
   switch (S.N) {
 #define RS_LANE(NN)                                                                             \

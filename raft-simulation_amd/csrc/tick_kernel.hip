@@ -192,12 +192,7 @@ hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st) {
 }
 
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
-                             hipStream_t st, bool dense) {
-  if (dense) {   // one slot per cluster, in key order (plan_chunk<1> never pads)
-    hipLaunchKernelGGL(sched_range_kernel<1>, dim3(SCHED_RANGE_BLOCKS), dim3(1024), 0, st, S, zero,
-                       perm, nslots);
-    return hipGetLastError();
-  }
+                             hipStream_t st) {
   switch (64 / S.N) {
 #define RS_PLAN(CPW)                                                                             \
   case CPW:                                                                                      \

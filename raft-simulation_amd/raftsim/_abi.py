@@ -133,6 +133,7 @@ _SIGS = {
     "read_counters": (C.c_int, [C.c_void_p, P(Counters)]),
     "digest": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint64)]),
     "last_step_timing": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32)]),
+    "last_span": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "destroy": (None, [C.c_void_p]),
     "last_error": (C.c_char_p, []),
 }

@@ -31,7 +31,7 @@ class Backend:
 
     def __init__(self, lib_path, prefix, **config):
         self._lib = C.CDLL(str(lib_path))
-        self._fns = _abi.bind(self._lib, prefix, optional=("last_step_timing",))
+        self._fns = _abi.bind(self._lib, prefix, optional=("last_step_timing", "last_span"))
         if self._fns["abi_version"]() != 2:
             raise RaftSimError("ABI version mismatch")
         self.config = make_config(self._fns, **config)
@@ -88,6 +88,12 @@ class Backend:
         ms, n = C.c_double(), C.c_uint32()
         self._check(self._fns["last_step_timing"](self._h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def last_span(self):
+        """Device ms of everything the last step (or the steps since the previous sync) enqueued."""
+        ms = C.c_double()
+        self._check(self._fns["last_span"](self._h, C.byref(ms)))
+        return ms.value
 
     # -- state ----------------------------------------------------------------------------------
     def read_nodes_raw(self, c0=0, nc=None):

@@ -57,3 +57,38 @@ def reduce_sum(x: float, device=None) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def reduce_min(x: int, device=None) -> int:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def first_violation_search(sim, chunk: int, max_ticks: int, reduce_min_fn=None):
+    """Step `sim` (any raftsim Backend) `chunk` ticks at a time until a safety violation has been
+    counted anywhere in the job (BASELINE config 5: time to the first violation). With
+    `reduce_min_fn` (a MIN all-reduce over the ranks, e.g. `lambda x: reduce_min(x, dev)`) every
+    rank stops after the same chunk: the one in which any rank first counted a violation.
+    Returns (job's first violation tick or None, ticks stepped, timing) with timing = (device ms
+    of the steps, summed tick-kernel ms, tick-kernel launches) on a GPU backend, zeros otherwise."""
+    done, span, kms, launches = 0, 0.0, 0.0, 0
+    timed = "last_span" in getattr(sim, "_fns", {})
+    fv = NONE_TICK
+    while done < max_ticks and fv == NONE_TICK:
+        n = min(chunk, max_ticks - done)
+        sim.step(n)
+        done += n
+        if timed:
+            span += sim.last_span()
+            ms, nl = sim.last_step_timing()
+            kms += ms * nl
+            launches += nl
+        fv = sim.counters()["first_violation_tick"]
+        fv = NONE_TICK if fv is None else int(fv)
+        if reduce_min_fn is not None:
+            fv = reduce_min_fn(fv)
+    return (None if fv == NONE_TICK else fv), done, (span, kms, launches)

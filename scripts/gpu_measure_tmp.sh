@@ -1,0 +1,8 @@
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 120 python -u scripts/lane_timeline.py raft-simulation_amd/build/libraftsim_wavelog.so 65536 6 > gpurun_out/timeline.txt 2>&1 || { echo "timeline failed"; tail gpurun_out/timeline.txt; exit 1; }
+cat gpurun_out/timeline.txt
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo "bench failed"; tail -30 gpurun_out/bench_full.err; exit 1; }
+echo bench ok
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/kt_c2 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload c2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/kt_c2.log 2>&1 || { echo "kt failed"; exit 1; }
+echo kt ok

@@ -153,12 +153,10 @@ def test_gpu_c2_full_size(seed):
     assert bails[0] == -1 and bails[-1] == 0, bails
 
 
-@pytest.mark.parametrize("pack", ["dense", "identity"])
-def test_gpu_c2_bench_window(pack, monkeypatch):
+def test_gpu_c2_bench_window():
     """The exact window bench.py times for C2: seed 42, 65,536 clusters, 2 warm-up then 20 timed
     10k-tick steps enqueued back to back (step_async + one sync), as the bench runs them;
     digest-equal to the oracle after the warm-up and at the end, every counter equal."""
-    monkeypatch.setenv("RAFTSIM_STEADY_PACK", pack)
     cfg = dict(n_clusters=65536, nodes=5, seed=42)
     g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
     helpers.oracle_threads(r, helpers.cpu_threads())
@@ -449,15 +447,13 @@ LITE_CASES = ["c2_small", "lite_n2", "lite_n3", "lite_n4", "lite_elections", "li
               "lite_odd_launches", "lite_short_round"]
 
 
-@pytest.mark.parametrize("pack", ["dense", "identity"])
 @pytest.mark.parametrize("name", LITE_CASES)
-def test_gpu_forced_steady_matches_oracle(name, pack, monkeypatch):
+def test_gpu_forced_steady_matches_oracle(name, monkeypatch):
     """Every LITE launch on the steady kernel (RAFTSIM_STEADY=always), from init-node: elections
     and every other event outside its model go through the workgroup's catch-up (the general
     tick body over the clusters it bailed, several wave slots per wave); GPU == oracle after
     every chunk."""
     monkeypatch.setenv("RAFTSIM_STEADY", "always")
-    monkeypatch.setenv("RAFTSIM_STEADY_PACK", pack)
     cfg = CASES[name]
     g, r = run_pair(cfg, 20000, 5000)
     assert g.counters() == r.counters()
