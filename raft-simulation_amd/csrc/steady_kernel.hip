@@ -363,24 +363,21 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
     }
     RS_LPH(2);
-    if (fae || round) {                      // append-entries-handler at each follower
-      // every follower's handler is computed and kept where it ran: the trace hashes are
-      // independent chains the compiler interleaves (in a round every follower answers the same
-      // heartbeat on the same tick)
-      const uint32_t ta = round ? t + d : t;
-      const uint32_t fa = round ? (1u << F) - 1 : fae;
+    // A trip runs exactly one of: a whole round (below), a heartbeat alone (its round did not fit:
+    // the append-entries are taken one tick later as `fae`), append-entries that arrived (fae),
+    // or queued responses (lres): a heartbeat with a follower still holding an append-entries,
+    // and append-entries with responses still queued, were bailed above.
+    auto append_entries = [&](uint32_t ta, uint32_t fa) {   // append-entries-handler, followers fa
 #pragma unroll
       for (int j = 0; j < F; ++j) {
-        const bool run_j = (fa >> j) & 1;
-        const uint32_t mterm = qT[j], rterm = fterm[j];
-        const bool ok = mterm >= fterm[j];
-        const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) | RAFT_FOLLWER |
-                                       Lid << 6
-                                 : ffl[j];
-        const uint32_t nterm = ok ? mterm : fterm[j];
-        const uint64_t ntr = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3,
-                                         nterm, 0);
-        if (run_j) {
+        if ((fa >> j) & 1) {
+          const uint32_t mterm = qT[j], rterm = fterm[j];
+          const bool ok = mterm >= fterm[j];
+          const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) |
+                                         RAFT_FOLLWER | Lid << 6
+                                   : ffl[j];
+          const uint32_t nterm = ok ? mterm : fterm[j];
+          ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3, nterm, 0);
           if (ok) {
             fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
             fmk[j] &= 0xFFFF0000u;
@@ -391,7 +388,6 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
           qA[j] = INF;
           fdl[j] = ta + S.el_base;                           // + the deferred draw
-          ftr[j] = ntr;
         }
       }
       fpend |= fa;
@@ -400,43 +396,53 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       resA = ta + d;
       nae += __popc(fa);
       tl = ta;
-    }
-    RS_LPH(3);
-    if (lres || round) {                     // append-response-handler, heads in sender order
-      // from tick tau0 one response per tick while nothing else in the cluster is due (the
-      // followers' next events and the launch end; the leader's own deadline moves past each):
-      // the decided response at t, or a round's responses from t + 2d. A response outside the
-      // model ends the run of responses and the next trip decides it.
-      const uint32_t tau0 = round ? t + 2 * d : t;
+    };
+    // append-response-handler for follower slot j's response at tick tau (core.clj:141-149);
+    // false (and nothing done) when it is outside the model: a newer term, a success response
+    // that would be checker work, or a failure without the peer's key (NPE)
+    auto response = [&](int j, uint32_t tau, uint32_t yT, uint32_t yA, uint32_t yB, uint32_t yH,
+                        int32_t& nxj, int32_t& mtj) {
+      const uint32_t yid = fk(j) + 1;
+      if (yT > Lterm || (yH ? ackbad : ((Lmk >> (16 + yid)) & 1) == 0)) return false;
+      rmask &= ~(1u << j);
+      Lmk |= yH << (16 + yid);
+      nxj = yH ? (int32_t)yB : nxj - 1;
+      mtj = yH ? (int32_t)yA : mtj;
+      Ldl = tau + S.hb;
+      Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, yid, yT, RAFT_LEADER, Lterm, 0);
+      ++nar;
+      tl = tau;
+      return true;
+    };
+    if (round) {
+      // every follower at t + d, then the responses at t + 2d .. t + 2d + F - 1 in slot order (the
+      // round's conditions put them all before the launch end and every follower's next event):
+      // straight-line code, every index static
+      append_entries(t + d, (1u << F) - 1);
+      bool go = true;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        go = go && response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
+      if (!rmask) resA = INF;
+    } else if (fae) {
+      append_entries(t, fae);
+    } else if (lres) {
+      // from t one response per tick, heads in sender order, while nothing else in the cluster
+      // is due (the followers' next events and the launch end; the leader's own deadline moves
+      // past each); the first one at t was decided above. A response outside the model ends the
+      // run and the next trip decides it.
       uint32_t E = tend;
 #pragma unroll
       for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
-      if (lres) E = max(E, t + 1);           // decided: the first response runs
-      for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
+      E = max(E, t + 1);
+      for (uint32_t tau = t; rmask && tau < E; ++tau) {
         const int h2 = __builtin_ctz(rmask);
-        uint32_t yT = 0, yA = 0, yB = 0, yH = 0;
+        bool ok = true;
 #pragma unroll
-        for (int j = 0; j < F; ++j) {
-          if (j == h2) {
-            yT = rT[j]; yA = rA[j]; yB = rB[j]; yH = rH[j];
-          }
-        }
-        const uint32_t yid = (uint32_t)h2 + 1 + ((uint32_t)h2 >= L ? 1u : 0u);
-        if (yT > Lterm || (yH ? ackbad : ((Lmk >> (16 + yid)) & 1) == 0)) break;
-        rmask &= rmask - 1;
+        for (int j = 0; j < F; ++j)
+          if (j == h2) ok = response(j, tau, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
+        if (!ok) break;
         if (!rmask) resA = INF;
-        Lmk |= yH << (16 + yid);
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          if (j == h2) {
-            nx[j] = yH ? (int32_t)yB : nx[j] - 1;
-            mt[j] = yH ? (int32_t)yA : mt[j];
-          }
-        }
-        Ldl = tau + S.hb;
-        Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, yid, yT, RAFT_LEADER, Lterm, 0);
-        ++nar;
-        tl = tau;
       }
     }
     RS_LPH(4);

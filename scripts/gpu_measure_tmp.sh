@@ -6,3 +6,8 @@ echo bench ok
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/kt_c2 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload c2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/kt_c2.log 2>&1 || { echo "kt failed"; exit 1; }
 echo kt ok
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python -u scripts/wavelog_probe.py raft-simulation_amd/build/libraftsim_wavelog.so 131072 c3 4 > gpurun_out/wl_c3.txt 2>&1 || { echo "wl c3 failed"; tail gpurun_out/wl_c3.txt; exit 1; }
+cat gpurun_out/wl_c3.txt
+timeout -k 10 200 python -u scripts/wavelog_probe.py raft-simulation_amd/build/libraftsim_wavelog.so 131072 c3_spec 4 > gpurun_out/wl_c3s.txt 2>&1 || { echo "wl c3s failed"; tail gpurun_out/wl_c3s.txt; exit 1; }
+cat gpurun_out/wl_c3s.txt

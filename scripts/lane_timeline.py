@@ -44,7 +44,7 @@ u, cnt = np.unique(key, return_counts=True)
 print("distinct SIMDs", len(u), "waves per SIMD p0/50/100", cnt.min(), np.median(cnt), cnt.max())
 ph = a[:, 12:17].astype(np.float64)
 trips = np.maximum(a[:, 4], 1)[:, None]
-names = ("head", "decide", "heartbeat", "responses", "append-entries")
+names = ("head", "decide", "heartbeat", "-", "run (append-entries + responses)")
 print("shader cycles per trip (mean over waves): " + "  ".join(
     f"{nm} {v:7.0f}" for nm, v in zip(names, (ph / trips).mean(axis=0))))
 print("shader cycles per wave (mean): " + "  ".join(f"{nm} {v:8.0f}" for nm, v in zip(names, ph.mean(axis=0))))
