@@ -349,12 +349,14 @@ constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 // words), for the N whose block then still fits four per CU.
 template <int N>
 constexpr bool nm_lds() { return N <= 5; }
-// TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key)
+// TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key);
+// DPEND_WORDS: per lane, 1 while its node's deadline is a deferred re-arm's lower bound
 constexpr int TRIP_WORDS = 64;
+constexpr int DPEND_WORDS = 64;
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
-         TRIP_WORDS;
+         TRIP_WORDS + DPEND_WORDS;
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -399,6 +401,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
   uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
   tripsL[lane] = 0;          // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
+  uint32_t* const dpend = tripsL + TRIP_WORDS;      // (likewise)
+  dpend[lane] = 0;
   __builtin_amdgcn_wave_barrier();
 
   // RAFT_SCHED_ALIGNED launches a grid sized for the padded packing; waves past its slots exit.
@@ -528,6 +532,12 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     wl_ts = __builtin_amdgcn_s_memtime();
     wl_ph[9] = (uint32_t)(wl_ts - wl_mt0);
   #endif
+    // A non-leader's re-armed timer (D4: t + el_base + the EVENT draw's word 1) is only compared
+    // with ticks at or past t + el_base, so its draw is deferred (dpend) unless the event drew
+    // anyway (the alts!! bit, a rand-nth redirect): the deadline holds that lower bound, which
+    // also serves as the cluster's next event; when a tick at or past it comes with no message
+    // ready (a message wins, D3, and in the faithful model its event re-arms the timer anyway) the
+    // draw is made in P1 and the timeout decided on the exact deadline, else at the write-back.
     for (;;) {
       uint32_t t = max(tnext, next_event());
       t = t < tend ? t : tend;
@@ -603,9 +613,17 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       bool elected = false, mchg = false;
       uint32_t pmax = 0;                                        // largest AE payload emitted
       uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
+      // A deferred timer draw due at this tick with no message ready: its own tick's draw
+      // (deadline - el_base) decides whether the node times out now.
+      if (!SPEC && live && dpend[lane] && !req_ok && !res_ok && n.deadline <= t) {
+        const uint4 wd = event_draw(sg, id, n.deadline - S.el_base, S);
+        n.deadline += __umulhi(wd.y, S.el_span);
+        dpend[lane] = 0;
+      }
       if (live && (req_ok || res_ok || t >= n.deadline)) {
-        // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready,
-        // and for the next timeout of a non-leader (core.clj:174); leaders' events skip it.
+        // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready;
+        // the next timeout of a non-leader (core.clj:174) takes it when there is one, else its
+        // draw is deferred (leaders' events need none).
         uint4 w = make_uint4(0, 0, 0, 0);
         bool have_w = false;
         int which = -1;
@@ -645,10 +663,6 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // sorted, so head == tail means all equal): then nothing this tick waits on memory.
           uint32_t narr = INF;
           if (q.c > 1) narr = (q.c == 2 || q.arr == q.tail) ? q.tail : qb[nh * qs];
-          if (!have_w && n.role != RAFT_LEADER) {
-            w = event_draw(sg, id, t, S);
-            have_w = true;
-          }
           QueueR r = q;
           r.h = nh;
           r.c -= 1;
@@ -866,11 +880,17 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // generate-timeout (core.clj:171-174) for the next wait: every event re-arms the timer
           // (D4); Spec-Raft keeps Raft's timers (SIM_SPEC §8)
           if (n.role == RAFT_LEADER) {
-            if (!SPEC || ev == 7 || elected) n.deadline = t + S.hb;
+            if (!SPEC || ev == 7 || elected) {
+              n.deadline = t + S.hb;
+              dpend[lane] = 0;
+            }
           } else if (!SPEC || ev == 6 || rearm || was_leader) {
-            if (!have_w) w = event_draw(sg, id, t, S);
-            have_w = true;
-            n.deadline = t + S.el_base + __umulhi(w.y, S.el_span);
+            // Spec-Raft re-arms on few events (SIM_SPEC §8): drawn at once there
+            if (SPEC && !have_w) w = event_draw(sg, id, t, S);
+            const bool defer = !SPEC && !have_w;
+            n.deadline = t + S.el_base + (defer ? 0u : __umulhi(w.y, S.el_span));
+            if (!SPEC) dpend[lane] = defer;                    // the draw is deferred
+            have_w = have_w || SPEC;
           }
           n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
           // leader-state words (cold, in HBM)
@@ -911,7 +931,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             } else {
               uint32_t dst = n.lid;
               if (!dst) {
-                if (!have_w) w = event_draw(sg, id, t, S);
+                if (!have_w) w = event_draw(sg, id, t, S);   // (the timer stays deferred)
                 const uint32_t i = __umulhi(w.z, N - 1);
                 dst = i + 1 < id ? i + 1 : i + 2;
               }
@@ -1330,6 +1350,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #endif
 
     // ---------------------------------------------------------------- write back
+    if (!SPEC && active && dpend[lane]) {       // every deadline exact before it is stored
+      const uint4 wd = event_draw(g, (uint32_t)k0 + 1, n.deadline - S.el_base, S);
+      n.deadline += __umulhi(wd.y, S.el_span);
+      dpend[lane] = 0;
+    }
     if (S.shist) {
       // RAFT_SCHED_ALIGNED: the cluster's packing key relative to the next launch, counted into the
       // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
