@@ -76,20 +76,27 @@ struct DevSim {
   uint32_t* bail_report;    // host-mapped word (the host picks the next launches' path from it)
 };
 
-// Fields of a cluster block (word f * N + k of the block is field f of node k); next_index of peer
-// id p is field HF_NEXT + p - 1, match_index field HF_NEXT + N + p - 1; the cluster's 8 words
-// start at hot_cl_off(N). Blocks are whole 128-B lines.
+// A cluster block: the cluster's 8 words (hot_cl_off = 0), then the node fields, field-major
+// (word HOT_CW + f * N + k is field f of node k): the HotField fields, next_index of peer id p as
+// field HF_NEXT + p - 1, match_index as HF_NEXT + N + p - 1, then the arena cursors and the
+// last-led term (hf_abase / hf_afront / hf_led). Blocks are whole 128-B lines. The order puts what
+// a steady-state launch writes -- every node's deadline and trace hash -- in one line (words 8-22
+// at N = 5), and everything the steady kernel reads in the first four lines (words 0-122).
+constexpr uint32_t HOT_CW = 8;
 enum HotField : uint32_t {
-  HF_FLAGS, HF_MASKS, HF_TERM, HF_COMMIT, HF_LEN, HF_DEADLINE, HF_QMETA, HF_REQ_ARR, HF_RES_ARR,
-  HF_REQ_TAIL, HF_RES_TAIL, HF_ABASE, HF_AFRONT, HF_LED, HF_TRACE_LO, HF_TRACE_HI, HF_NEXT
+  HF_DEADLINE, HF_TRACE_LO, HF_TRACE_HI, HF_QMETA, HF_REQ_ARR, HF_RES_ARR, HF_REQ_TAIL,
+  HF_RES_TAIL, HF_FLAGS, HF_MASKS, HF_TERM, HF_COMMIT, HF_LEN, HF_NEXT
 };
-__host__ __device__ constexpr uint32_t hot_cl_off(uint32_t N) { return (HF_NEXT + 2 * N) * N; }
+__host__ __device__ constexpr uint32_t hf_abase(uint32_t N) { return HF_NEXT + 2 * N; }
+__host__ __device__ constexpr uint32_t hf_afront(uint32_t N) { return HF_NEXT + 2 * N + 1; }
+__host__ __device__ constexpr uint32_t hf_led(uint32_t N) { return HF_NEXT + 2 * N + 2; }
+__host__ __device__ constexpr uint32_t hot_cl_off(uint32_t) { return 0; }
 __host__ __device__ constexpr uint32_t hot_block_words(uint32_t N) {
-  return (hot_cl_off(N) + 8 + 31) & ~31u;
+  return (HOT_CW + (hf_led(N) + 1) * N + 31) & ~31u;
 }
 // Word 0 of node k's fields in cluster c's block (field f at [f * N]) / the cluster's 8 words.
 __device__ __forceinline__ uint32_t* hot_node(const DevSim& S, uint32_t c, uint32_t k) {
-  return S.hot + (size_t)c * S.HB + k;
+  return S.hot + (size_t)c * S.HB + HOT_CW + k;
 }
 __device__ __forceinline__ uint32_t* hot_cl(const DevSim& S, uint32_t c) {
   return S.hot + (size_t)c * S.HB + hot_cl_off(S.N);

@@ -407,7 +407,7 @@ static size_t qpitch(Shard* s, uint32_t which) {
 
 // Field `f` of node `id` in cluster `cluster`'s hot block (rs::HotField).
 static uint32_t* hot_word(Shard* s, uint32_t cluster, uint32_t id, uint32_t f) {
-  return s->d.hot + (size_t)cluster * s->d.HB + (size_t)f * s->N + (id - 1);
+  return s->d.hot + (size_t)cluster * s->d.HB + rs::HOT_CW + (size_t)f * s->N + (id - 1);
 }
 static uint32_t* cl_words(Shard* s, uint32_t cluster) {
   return s->d.hot + (size_t)cluster * s->d.HB + rs::hot_cl_off(s->N);
@@ -439,7 +439,7 @@ static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
   HIP_OK(d2h(s, cc.data(), s->d.ccount + n0, cnt));
   HIP_OK(hipStreamSynchronize(s->stream));
   for (size_t i = 0; i < cnt; ++i) {
-    const uint32_t* h = &blk[(i / N) * HB + i % N];     // field f at h[f * N]
+    const uint32_t* h = &blk[(i / N) * HB + rs::HOT_CW + i % N];     // field f at h[f * N]
     auto f = [&](uint32_t fld) { return h[fld * N]; };
     raft_node_t& r = out[i];
     memset(&r, 0, sizeof r);
@@ -453,8 +453,8 @@ static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
       r.next_index[p] = (int32_t)f(rs::HF_NEXT + p);
       r.match_index[p] = (int32_t)f(rs::HF_NEXT + N + p);
     }
-    r.last_led_term = f(rs::HF_LED);
-    r.arena_base = f(rs::HF_ABASE); r.arena_frontier = f(rs::HF_AFRONT);
+    r.last_led_term = f(rs::hf_led(N));
+    r.arena_base = f(rs::hf_abase(N)); r.arena_frontier = f(rs::hf_afront(N));
     r.req_count = (qm >> 4) & 31; r.res_count = (qm >> 13) & 31;
     r.trace_hash = (uint64_t)f(rs::HF_TRACE_HI) << 32 | f(rs::HF_TRACE_LO);
     r.commit_count = cc[i];
@@ -488,15 +488,15 @@ static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t*
   HIP_OK(hipStreamSynchronize(s->stream));
   for (size_t i = 0; i < cnt; ++i) {
     const raft_node_t& r = in[i];
-    uint32_t* h = &blk[(i / N) * HB + i % N];
+    uint32_t* h = &blk[(i / N) * HB + rs::HOT_CW + i % N];
     auto f = [&](uint32_t fld) -> uint32_t& { return h[fld * N]; };
     f(rs::HF_FLAGS) = rs::pack_flags(r.role, r.voted_for, r.leader_id, r.fault, r.entries_is_seq,
                                      r.ls_present);
     f(rs::HF_MASKS) = r.votes | (uint32_t)r.ls_keys << 16;
     f(rs::HF_TERM) = r.current_term; f(rs::HF_COMMIT) = r.commit_index;
     f(rs::HF_LEN) = r.log_len; f(rs::HF_DEADLINE) = r.deadline;
-    f(rs::HF_ABASE) = r.arena_base; f(rs::HF_AFRONT) = r.arena_frontier;
-    f(rs::HF_LED) = r.last_led_term;
+    f(rs::hf_abase(N)) = r.arena_base; f(rs::hf_afront(N)) = r.arena_frontier;
+    f(rs::hf_led(N)) = r.last_led_term;
     f(rs::HF_TRACE_LO) = (uint32_t)r.trace_hash; f(rs::HF_TRACE_HI) = (uint32_t)(r.trace_hash >> 32);
     ccv[i] = r.commit_count;
     for (size_t p = 0; p < N; ++p) {

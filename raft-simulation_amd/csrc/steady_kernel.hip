@@ -60,7 +60,12 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   static_assert(N >= 2 && N <= 5, "follower masks and the response queue fit four followers");
   constexpr int F = N - 1;
   constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
-  constexpr int NW4 = (int)(CLW + 4) / 4;          // uint4s up to and including the checker hwm
+  // the words read: the cluster's (checker hwm) and every node field up to the leader-state rows
+  // (device.hpp: words 0-122 at N = 5, four lines), loaded at once -- the leader's rows are picked
+  // from them once its id is known, with no second round trip
+  constexpr int NWORDS = (int)(HOT_CW + hf_abase(N) * N);
+  constexpr int NW4 = (NWORDS + 3) / 4;
+  static_assert(CLW == 0, "the cluster words lead the block");
   __shared__ uint32_t sctr[4];
   __shared__ uint32_t nbl;                         // clusters this workgroup bailed
   __shared__ uint32_t bl_c[LANE_WG], bl_t[LANE_WG];   // bailed cluster, tick it stopped before
@@ -96,26 +101,20 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #define RS_LPH(i) do {} while (0)
 #endif
 
-  // ------------------------------------------- load: fields FLAGS..RES_TAIL, TRACE, checker hwm
+  // ------------------------------------------- load: the checker hwm and fields up to the rows
   uint32_t w[NW4 * 4];
 #pragma unroll
   for (int i = 0; i < NW4 * 4; ++i) w[i] = 0;
   if (active) {
 #pragma unroll
     for (int i = 0; i < NW4; ++i) {
-      const int lo = 4 * i, hi = 4 * i + 3;
-      const bool need = lo < (int)(HF_ABASE * N) ||
-                        (hi >= (int)(HF_TRACE_LO * N) && lo < (int)(HF_NEXT * N)) ||
-                        (lo <= (int)CLW && hi >= (int)CLW);
-      if (need) {
-        const uint4 x = reinterpret_cast<const uint4*>(blk)[i];
-        w[lo] = x.x; w[lo + 1] = x.y; w[lo + 2] = x.z; w[lo + 3] = x.w;
-      }
+      const uint4 x = reinterpret_cast<const uint4*>(blk)[i];
+      w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
     }
   }
   auto field = [&](int f, uint32_t (&out)[N]) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) out[k] = w[f * N + k];
+    for (int k = 0; k < N; ++k) out[k] = w[HOT_CW + f * N + k];
   };
   uint32_t nfl[N], nqm[N];
   field(HF_FLAGS, nfl);
@@ -172,10 +171,20 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   }
   // the leader's rows for its followers: next_index / match_index of peer id fk(j) + 1
   int32_t nx[F], mt[F];
+  {
+    uint32_t rn[N], rm[N];                    // the leader's next / match of each peer id p + 1
 #pragma unroll
-  for (int j = 0; j < F; ++j) {
-    nx[j] = active ? (int32_t)blk[(HF_NEXT + fk(j)) * N + L] : 0;
-    mt[j] = active ? (int32_t)blk[(HF_NEXT + N + fk(j)) * N + L] : 0;
+    for (int p = 0; p < N; ++p) {
+      field(HF_NEXT + p, tmp);
+      rn[p] = pick<N>(tmp, L);
+      field(HF_NEXT + N + p, tmp);
+      rm[p] = pick<N>(tmp, L);
+    }
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      nx[j] = (int32_t)fsel(rn, j);
+      mt[j] = (int32_t)fsel(rm, j);
+    }
   }
   int32_t nx0[F], mt0[F];                     // as loaded: unchanged words are not stored back
 #pragma unroll
@@ -470,8 +479,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
   }
   if (wb) {
-    // every word of fields FLAGS..RES_TAIL and TRACE_LO/HI, from registers (LEN unchanged)
-    constexpr int NV = 16;
+    // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
+    constexpr int NV = HF_NEXT;
     uint32_t v[NV][N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
@@ -499,16 +508,14 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       v[HF_TRACE_LO][k] = (uint32_t)tr;
       v[HF_TRACE_HI][k] = (uint32_t)(tr >> 32);
     }
-    auto live = [](int q) {
-      return q < (int)(HF_ABASE * N) || (q >= (int)(HF_TRACE_LO * N) && q < (int)(HF_NEXT * N));
-    };
-    auto val = [&](int q) { return v[q / N][q % N]; };
-    // Only words that changed are stored (in a heartbeat round the deadlines and trace hashes do;
-    // flags, terms, masks, commits, queue words and rows come back unchanged): a lane's stores
-    // each go to a different cluster's block, one L2 request per lane, and the write-back of the
-    // whole grid at the launch end is bound by that request rate.
+    auto live = [](int q) { return q >= (int)HOT_CW && q < (int)(HOT_CW + HF_NEXT * N); };
+    auto val = [&](int q) { return v[(q - HOT_CW) / N][(q - HOT_CW) % N]; };
+    // Only words that changed are stored (in a heartbeat round the deadlines and trace hashes do,
+    // all in the block's first line; flags, terms, masks, commits, queue words and rows come back
+    // unchanged): a lane's stores each go to a different cluster's block, and every dirty line is
+    // written back at the launch end.
 #pragma unroll
-    for (int i = 0; i < (int)(HF_NEXT * N + 3) / 4; ++i) {
+    for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_NEXT * N + 3) / 4; ++i) {
       const int lo = 4 * i;
       if (live(lo) && live(lo + 1) && live(lo + 2) && live(lo + 3)) {
         if (val(lo) != w[lo] || val(lo + 1) != w[lo + 1] || val(lo + 2) != w[lo + 2] ||
@@ -524,8 +531,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     // the leader's rows (node L): next / match of peer fk(j) + 1
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      if (nx[j] != nx0[j]) blk[(HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
-      if (mt[j] != mt0[j]) blk[(HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
+      if (nx[j] != nx0[j]) blk[HOT_CW + (HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
+      if (mt[j] != mt0[j]) blk[HOT_CW + (HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
     }
     // queues back to the rings, heads at slot 0
 #pragma unroll

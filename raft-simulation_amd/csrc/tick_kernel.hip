@@ -9,9 +9,12 @@ namespace rs {
 
 // The general tick kernel: one wave per workgroup (wave lifetimes differ by up to 2x under load,
 // and a multi-wave workgroup holds its CU slot and LDS until its slowest wave ends; measured:
-// 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound.
+// 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound. At
+// N <= 5 the compiler is asked for 4 waves per SIMD (<= 128 VGPRs), which it meets without
+// spilling (unasked it took 129 for the Spec-Raft form); at N >= 6 that would spill.
 template <int N, bool TRACE, bool SPEC, bool LITE>
-__global__ void __launch_bounds__(64) tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 5 && !TRACE ? 4 : 1, 8)))
+tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   tick_wave<N, TRACE, SPEC, LITE>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x, gridDim.x, S.perm,
                                   S.perm ? *S.nslots : S.C, nullptr, blockIdx.x);
@@ -214,7 +217,7 @@ __global__ void init_kernel(DevSim S) {
   const uint4 w = philox(S.goff + c, id | P_INIT << 8, 0, 0, S.key0, S.key1);
   uint32_t* h = hot_node(S, c, id - 1);
   const uint32_t N = S.N;
-  for (uint32_t f = 0; f < HF_NEXT + 2 * N; ++f) h[f * N] = 0;    // incl. next / match
+  for (uint32_t f = 0; f <= hf_led(N); ++f) h[f * N] = 0;          // incl. next / match
   h[HF_TERM * N] = 1;
   h[HF_DEADLINE * N] = S.el_base + __umulhi(w.y, S.el_span);
   h[HF_REQ_ARR * N] = INF; h[HF_RES_ARR * N] = INF;
@@ -249,11 +252,11 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
                             hw[HF_DEADLINE * N]};
     for (int i = 0; i < 12; ++i) h = fnv(h, w[i]);
     for (uint32_t p = 0; p < 2 * N; ++p) h = fnv(h, hw[(HF_NEXT + p) * N]);   // next, then match
-    h = fnv(h, hw[HF_LED * N]);
+    h = fnv(h, hw[hf_led(N) * N]);
     h = fnv(h, hw[HF_TRACE_LO * N]);
     h = fnv(h, hw[HF_TRACE_HI * N]);
-    h = fnv(h, hw[HF_ABASE * N]);
-    h = fnv(h, hw[HF_AFRONT * N]);
+    h = fnv(h, hw[hf_abase(N) * N]);
+    h = fnv(h, hw[hf_afront(N) * N]);
     const uint32_t cc = S.ccount[gi];
     h = fnv(h, cc);
     if (S.SC) {
@@ -287,7 +290,7 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
       }
     }
     const uint2* ar = arena_of(S, gi);
-    const uint32_t base = hw[HF_ABASE * N], len = hw[HF_LEN * N];
+    const uint32_t base = hw[hf_abase(N) * N], len = hw[HF_LEN * N];
     for (uint32_t i = 0; i < len; ++i) {
       const uint2 e = ar[(base + i) % S.A];
       h = fnv(h, e.x);

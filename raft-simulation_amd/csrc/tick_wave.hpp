@@ -421,7 +421,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     const uint32_t A = S.A;
     constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
     // this node's words in its cluster's block (field f at hp[f * N]) and the cluster's words
-    uint32_t* const hp = S.hot + (size_t)c * HB + k0;
+    uint32_t* const hp = S.hot + (size_t)c * HB + HOT_CW + k0;
     uint32_t* const hc = S.hot + (size_t)c * HB + CLW;
 
     NodeR n = {};
@@ -437,7 +437,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
       n.rq.arr = hp[HF_REQ_ARR * N]; n.rs.arr = hp[HF_RES_ARR * N];
       n.rq.tail = hp[HF_REQ_TAIL * N]; n.rs.tail = hp[HF_RES_TAIL * N];
-      n.base = hp[HF_ABASE * N]; n.front = hp[HF_AFRONT * N]; n.led = hp[HF_LED * N];
+      n.base = hp[hf_abase(N) * N]; n.front = hp[hf_afront(N) * N]; n.led = hp[hf_led(N) * N];
       n.trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
       hidx = hc[0]; hterm = hc[1]; hval = hc[2]; cnext = hc[3]; ccount = hc[4];
       if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
@@ -559,7 +559,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       uint32_t* const mycells = cells + bl * (N - 1) * CELLW;
       uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
       uint2* const sar = arena_of(S, sgi);
-      int32_t* const hnm = reinterpret_cast<int32_t*>(S.hot + (size_t)(sg - S.goff) * HB + k);
+      int32_t* const hnm = reinterpret_cast<int32_t*>(S.hot + (size_t)(sg - S.goff) * HB + HOT_CW + k);
       const PeerW lsw = nm_lds<N>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
                                    : PeerW{hnm + HF_NEXT * N, hnm + (HF_NEXT + N) * N, (uint32_t)N};
       if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
@@ -1132,16 +1132,25 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         }
         if (__ballot(appended_at >= 0)) {              // log matching
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
+          // Transposed: for each node a that appended, every peer lane compares its own log with
+          // a's new entries at once (the peers' loads are in flight together, one memory round
+          // trip per W positions instead of one per peer), and a counts one violation if any
+          // peer found a position with the same term and another value.
           bool bad = false;
-  #pragma unroll
-          for (int s = 0; s < N; ++s) {
-            const uint32_t sb = __shfl(n.base, bl + s), sl = __shfl(n.len, bl + s);
-            if (appended_at >= 0 && s != k && !bad) {
-              const uint2* oa = arena_of(S, sgi - k + s);
-              const uint32_t hi = n.len < sl ? n.len : sl, lo = (uint32_t)appended_at;
+  #pragma unroll 1
+          for (int a = 0; a < N; ++a) {
+            const int32_t aat = __shfl(appended_at, bl + a);
+            if (!__ballot(active && aat >= 0)) continue;
+            const uint32_t ab = __shfl(n.base, bl + a), al = __shfl(n.len, bl + a);
+            bool c = false;
+            if (active && aat >= 0 && a != k) {
+              const uint32_t hi = al < n.len ? al : n.len, lo = (uint32_t)aat;
               if (hi > lo)
-                bad = log_conflict<LITE ? 1 : 4>(sar, (n.base + lo) % A, oa, (sb + lo) % A, hi - lo, A);
+                c = log_conflict<LITE ? 1 : 4>(arena_of(S, sgi - k + a), (ab + lo) % A, sar,
+                                               (n.base + lo) % A, hi - lo, A);
             }
+            const bool any = cluster_any(c);           // (a wave-wide ballot: every lane)
+            bad |= a == k && any;
           }
           if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
         }
@@ -1393,7 +1402,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       hp[HF_QMETA * N] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);
       hp[HF_REQ_ARR * N] = n.rq.arr; hp[HF_RES_ARR * N] = n.rs.arr;
       hp[HF_REQ_TAIL * N] = n.rq.tail; hp[HF_RES_TAIL * N] = n.rs.tail;
-      hp[HF_ABASE * N] = n.base; hp[HF_AFRONT * N] = n.front; hp[HF_LED * N] = n.led;
+      hp[hf_abase(N) * N] = n.base; hp[hf_afront(N) * N] = n.front; hp[hf_led(N) * N] = n.led;
       hp[HF_TRACE_LO * N] = (uint32_t)n.trace; hp[HF_TRACE_HI * N] = (uint32_t)(n.trace >> 32);
       if constexpr (nm_lds<N>()) {
   #pragma unroll
