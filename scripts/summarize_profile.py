@@ -27,9 +27,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 KERNEL = "tick_kernel"
-# LITE launches: the steady kernel (lane-per-cluster form, or the wave form), then the catch-up
-# tick kernel
-STEADY = ("steady_lane_kernel", "steady_kernel")
+# LITE launches on the steady path: the steady kernel, whose workgroups run the clusters they hand
+# over through the general tick body in the same dispatch
+STEADY = ("steady_lane_kernel",)
 
 
 def is_steady(name):
@@ -37,19 +37,8 @@ def is_steady(name):
 
 
 def launch_groups(rows, name_key):
-    """Group dispatch-ordered rows into tick launches: a steady_kernel dispatch together with the
-    catch-up tick_kernel dispatch that follows it, or one tick_kernel dispatch."""
-    groups = []
-    for r in rows:
-        nm = r[name_key]
-        if is_steady(nm):
-            groups.append([r])
-        elif KERNEL in nm:
-            if groups and len(groups[-1]) == 1 and is_steady(groups[-1][0][name_key]):
-                groups[-1].append(r)
-            else:
-                groups.append([r])
-    return groups
+    """Dispatch-ordered rows as tick launches: one dispatch each (steady or general)."""
+    return [[r] for r in rows if is_steady(r[name_key]) or KERNEL in r[name_key]]
 
 
 def counters_by_kernel(path):
@@ -83,12 +72,13 @@ def calibration(src):
 
 
 def vgpr_compiler(tag, n):
-    """VGPRs of the tick-kernel instantiations at N = n from profiles/TAG_kernel_resources.txt."""
+    """VGPRs of the tick and steady kernel instantiations at N = n from
+    profiles/TAG_kernel_resources.txt (the compiler's own counts)."""
     f = ROOT / "profiles" / f"{tag}_kernel_resources.txt"
     if not f.exists():
         return None
     return {l[:48].strip(): int(l.split()[-4]) for l in f.read_text().splitlines()
-            if l.startswith(f"tick_kernel<N={n},")}
+            if l.startswith((f"tick_kernel<N={n},", f"steady_lane_kernel<N={n}>"))}
 
 
 def main():
@@ -152,17 +142,17 @@ def main():
     k_wr = w_state * cal["wr_u32_contig"]["k_span"] + (1 - w_state) * cal["wr_msg32_contig"]["k_span"]
     fetch_raw, write_raw = avg.get("FETCH_SIZE", 0) * 1024, avg.get("WRITE_SIZE", 0) * 1024
     hbm = fetch_raw / k_rd + write_raw / k_wr
-    event_bytes = roof["bytes_per_launch"]
-    achieved = event_bytes / (avg_ns * 1e-9) / 1e9
+    state_bytes = roof["bytes_per_launch"]           # compulsory: the hot state in and out
+    event_bytes = roof["event_bytes_per_launch"]
+    achieved = state_bytes / (avg_ns * 1e-9) / 1e9
     out = {
         "tag": tag, "workload": wl, "kernel_src_sha": roof["kernel_src_sha"],
         "kernel": [r["Kernel_Name"] for r in groups[-1]] if groups else None,
         "launches_traced": len(durs), "avg_duration_ns_trace": avg_ns,
         "avg_duration_ns_per_kernel_stats": {r["Name"]: float(r["AverageNs"]) for r in stats},
-        "launch_note": "a LITE launch is the steady kernel then the catch-up tick kernel; its "
-                       "duration runs from the first dispatch's start to the last one's end "
-                       "(the span the bench's HIP events time) and its PMC counts are the sum "
-                       "over both dispatches",
+        "launch_note": "one dispatch per launch: the general tick kernel, or on the steady "
+                       "path the steady kernel, which runs the clusters it hands over in the "
+                       "same dispatch",
         "bench_avg_launch_ms_hip_events": roof["avg_launch_ms"],
         # rocprofv3's VGPR_Count field is the allocation granule count of another encoding; the
         # compiler's own register count is in profiles/TAG_kernel_resources.txt
@@ -191,14 +181,17 @@ def main():
         "hbm_fetch_bytes_raw": fetch_raw, "hbm_write_bytes_raw": write_raw,
         "hbm_bytes_per_launch": hbm,
         "roofline_recomputed": {
+            "compulsory_bytes_per_launch": state_bytes,
             "event_bytes_per_launch": event_bytes,
             "event_bytes_terms": {"state_in_out": 2 * (32 + 8 * n) * nodes,
                                   "messages_64B": 64 * cnt.get("delivered", 0) / launches,
                                   "entries_16B": 16 * cnt.get("entries_appended", 0) / launches},
             "achieved_GBs": achieved, "peak_GBs": 8000.0, "frac": achieved / 8000.0,
+            "frac_event_model": event_bytes / (avg_ns * 1e-9) / 1e9 / 8000.0,
+            "traffic_over_compulsory": hbm / state_bytes if state_bytes else None,
             "traffic_over_event_bytes": hbm / event_bytes if event_bytes else None,
-            "how": "event_bytes_per_launch / avg_duration_ns_trace; event bytes from the bench "
-                   "line's counters (bench_line below)"},
+            "how": "compulsory_bytes_per_launch / avg_duration_ns_trace (frac_event_model: the "
+                   "event bytes, from the bench line's counters, bench_line below)"},
         "bench_line": bench,
     }
     (dst / f"{tag}_{wl}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
@@ -211,6 +204,8 @@ def main():
     # same window (a C3 window from init-node changes cost per launch as nodes halt)
     traffic[wl] = {"hbm_bytes_per_launch": hbm, "kernel_src_sha": roof["kernel_src_sha"],
                    "window": bench.get("window"), "event_bytes_per_launch": event_bytes,
+                   "compulsory_bytes_per_launch": state_bytes,
+                   "traffic_over_compulsory": hbm / state_bytes if state_bytes else None,
                    "traffic_over_event_bytes": hbm / event_bytes if event_bytes else None,
                    "source": f"profiles/{tag}_{wl}_pmc.json"}
     tf.write_text(json.dumps(traffic, indent=1, sort_keys=True) + "\n")
