@@ -1150,7 +1150,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                                                (n.base + lo) % A, hi - lo, A);
             }
             const bool any = cluster_any(c);           // (a wave-wide ballot: every lane)
-            bad |= a == k && any;
+            bad |= active && a == k && any;            // (idle lanes past the clusters alias one)
           }
           if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
         }
