@@ -433,6 +433,38 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       for (int j = 0; j < F; ++j)
         go = go && response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
       if (!rmask) resA = INF;
+      // A round that ran every response leaves the cluster in its fixed point: every follower
+      // took the append-entries (its flags, votes, term and commit are what another one sets
+      // again) and every response succeeded (next / match / keys as another one sets them). If
+      // the followers' re-armed timers (>= t_ae + el_base) cannot fire before the next round's
+      // append-entries (el_base >= the round period P), the next heartbeat (last response + hb) is
+      // the cluster's next event, and every later round that ends before the launch does is
+      // this one shifted by a multiple of P: only the ticks in the trace hashes change. Those
+      // rounds run here as hashes alone, with the state and counters of the last one.
+      const uint32_t P = 2 * d + F - 1 + S.hb;
+      if (!rmask && S.el_base >= P && tend - t > P + 2 * d + F) {
+        const uint32_t R = (tend - t - 2 * d - F - 1) / P;       // more rounds that end in time
+        uint32_t tk = t;
+        for (uint32_t r = 0; r < R; ++r) {
+          tk += P;
+          Ltr = trace_event(Ltr, tk, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+#pragma unroll
+          for (int j = 0; j < F; ++j)
+            ftr[j] = trace_event(ftr[j], tk + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
+                                 Lterm, 0);
+#pragma unroll
+          for (int j = 0; j < F; ++j)
+            Ltr = trace_event(Ltr, tk + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
+                              RAFT_LEADER, Lterm, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < F; ++j) fdl[j] = tk + d + S.el_base;   // deferred draws (fpend)
+        Ldl = tk + 2 * d + F - 1 + S.hb;
+        tl = tk + 2 * d + F - 1;
+        nhb += R;
+        nae += F * R;
+        nar += F * R;
+      }
     } else if (fae) {
       append_entries(t, fae);
     } else if (lres) {

@@ -338,6 +338,16 @@ __device__ __forceinline__ void spec_handle(
   }
 }
 
+// The wave's lanes that hold node index a (lane l is node l mod N of cluster l / N; lanes past the
+// wave's whole clusters are idle).
+template <int N>
+__device__ __forceinline__ uint64_t node_lanes(int a) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int c = 0; c < 64 / N; ++c) m |= 1ull << (c * N);
+  return m << a;
+}
+
 // LDS words per wave: pair cells [cluster][sender][receiver other than the sender] of CELLW
 // words, then sender records [cluster][sender] of SRECW words, counters, and (Spec-Raft) the
 // wave's pre-tick arena frontiers.
@@ -1137,10 +1147,13 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // trip per W positions instead of one per peer), and a counts one violation if any
           // peer found a position with the same term and another value.
           bool bad = false;
+          // node indices a that appended in some cluster of the wave (lane l is node l mod N of
+          // its cluster): the others are skipped with scalar tests only
+          const uint64_t apm = __ballot(active && appended_at >= 0);
   #pragma unroll 1
           for (int a = 0; a < N; ++a) {
+            if (!(apm & node_lanes<N>(a))) continue;
             const int32_t aat = __shfl(appended_at, bl + a);
-            if (!__ballot(active && aat >= 0)) continue;
             const uint32_t ab = __shfl(n.base, bl + a), al = __shfl(n.len, bl + a);
             bool c = false;
             if (active && aat >= 0 && a != k) {
