@@ -30,7 +30,6 @@ constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min v
 constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
 static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
-constexpr int PW_WORDS = 64;    // 32 x u64 client-gap powers at the start of the block's LDS
 // Waves flush their counters into one of CTR_COPIES copies of the counter block (wave index mod
 // CTR_COPIES): thousands of waves ending together otherwise serialise on the same few words of
 // device-scope atomics (C2: 5,724 waves x up to 30 counters). The host reduces the copies.
@@ -39,10 +38,29 @@ constexpr int CTR_COPIES = 64;
 // the largest append-entries payload (MAX over waves)
 constexpr int CTR_STRIDE = RAFT_CTR_COUNT + 2;
 
+// Exact unsigned division by a launch-invariant d >= 1 (Granlund & Montgomery, round-up variant):
+// one v_mul_hi_u32 and a few shifts instead of the ~20-instruction division sequence, for every
+// 32-bit x. The client schedule divides by its period and burst and the partition draw by its
+// epoch on every injection and emission.
+struct DivU32 {
+  uint32_t d, m, s1, s2;
+};
+inline DivU32 make_div(uint32_t d) {
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;
+  return {d, (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1), l < 1 ? l : 1u,
+          l > 1 ? l - 1 : 0u};
+}
+__device__ __forceinline__ uint32_t udiv(const DivU32& v, uint32_t x) {
+  const uint32_t t1 = __umulhi(v.m, x);
+  return (t1 + ((x - t1) >> v.s1)) >> v.s2;
+}
+
 struct DevSim {
   uint32_t C, N, Q, L, A, NN, goff, key0, key1;
   uint32_t hb, el_base, el_span, drop_ppm, dup_ppm, dmin, dmax, part_ppm, part_epoch,
       client_ppm, variant, client_period, client_burst, client_redirects;
+  DivU32 div_period, div_burst, div_epoch;   // client_period (when > 0), client_burst, part_epoch
   uint32_t* hot;          // [C][HB] cluster blocks (HotField, hot_cl_off, hot_block_words)
   uint32_t HB;            // hot_block_words(N)
   uint32_t* qbuf;         // REQ [Q][NN][8], then RES [NN][Q][8]
@@ -159,6 +177,7 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
 // are 0 and never fire). The accumulator starts at 2^32 and every power is below 2^32 when
 // client_ppm > 0, so after its first step it fits 32 bits and (acc * pw) >> 32 is one
 // v_mul_hi_u32 instead of a 64x64-bit product.
+// pw is the kernel argument's table: the loop index is uniform, so each power is a scalar load.
 __device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
   // client_ppm == 0 (top == 32; reachable only through a host-written client cursor): every
   // power is 2^32, so the search takes every step
@@ -182,17 +201,19 @@ __device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, 
 // The client schedule (SIM_SPEC §4 P0, D14): bursts of B on-ticks at the start of every period P
 // (P = 0: every tick is on). Injections are spaced by geometric gaps counted in on-ticks: the tick
 // of on-tick number j, saturating at 2^32 - 1 = never (j >= 2^32 is never, as tick(j) >= j).
-__device__ inline uint32_t on_tick(uint64_t j, uint32_t P, uint32_t B) {
+__device__ inline uint32_t on_tick(uint64_t j, uint32_t P, const DivU32& B) {
   if (j >= 0xFFFFFFFFull) return 0xFFFFFFFFu;
   const uint32_t j32 = (uint32_t)j;
-  const uint64_t t = P ? (uint64_t)(j32 / B) * P + j32 % B : j32;
+  const uint32_t q = P ? udiv(B, j32) : 0u;
+  const uint64_t t = P ? (uint64_t)q * P + (j32 - q * B.d) : j32;
   return t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
 }
 // The next injection after the one at tick t (an on-tick), drawing gap word w.
-__device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const unsigned long long* pw,
-                                            int top, uint32_t P, uint32_t B) {
-  const uint64_t j = P ? (uint64_t)(t / P) * B + t % P : t;
-  return on_tick(j + 1 + client_gap(w, pw, top), P, B);
+__device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const DevSim& S) {
+  const uint32_t P = S.client_period;
+  const uint32_t q = P ? udiv(S.div_period, t) : 0u;
+  const uint64_t j = P ? (uint64_t)q * S.div_burst.d + (t - q * P) : t;
+  return on_tick(j + 1 + client_gap(w, S.client_pw, S.client_top), P, S.div_burst);
 }
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;

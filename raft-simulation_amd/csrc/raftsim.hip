@@ -189,6 +189,9 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   d.variant = cfg->variant_flags;
   d.client_period = cfg->client_period; d.client_burst = cfg->client_burst;
   d.client_redirects = cfg->client_redirects;
+  d.div_period = rs::make_div(cfg->client_period ? cfg->client_period : 1);
+  d.div_burst = rs::make_div(cfg->client_burst ? cfg->client_burst : 1);
+  d.div_epoch = rs::make_div(cfg->part_epoch);
   d.SC = cfg->commit_stream_cap;
   d.TC = cfg->trace_cap;
   d.TE = cfg->trace_entry_cap;

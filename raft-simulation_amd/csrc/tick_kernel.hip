@@ -9,11 +9,11 @@ namespace rs {
 
 // The general tick kernel: one wave per workgroup (wave lifetimes differ by up to 2x under load,
 // and a multi-wave workgroup holds its CU slot and LDS until its slowest wave ends; measured:
-// 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound. At
-// N <= 5 the compiler is asked for 4 waves per SIMD (<= 128 VGPRs), which it meets without
-// spilling (unasked it took 129 for the Spec-Raft form); at N >= 6 that would spill.
+// 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound. The
+// compiler is asked for 4 waves per SIMD (<= 128 VGPRs) where it meets that without spilling:
+// N <= 5, and the faithful kernels up to N = 8 (unasked it took 129 for some of them).
 template <int N, bool TRACE, bool SPEC, bool LITE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 5 && !TRACE ? 4 : 1, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(!TRACE && (N <= 5 || (!SPEC && N <= 8)) ? 4 : 1, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   tick_wave<N, TRACE, SPEC, LITE>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x, gridDim.x, S.perm,
@@ -227,8 +227,7 @@ __global__ void init_kernel(DevSim S) {
     uint32_t first = INF;
     if (S.client_ppm) {
       const uint4 d = philox(S.goff + c, P_CLIENT << 8, 0, 1, S.key0, S.key1);
-      first = on_tick(client_gap(d.x, S.client_pw, S.client_top), S.client_period,
-                      S.client_burst);
+      first = on_tick(client_gap(d.x, S.client_pw, S.client_top), S.client_period, S.div_burst);
     }
     uint32_t* cw = hot_cl(S, c);
     for (int i = 0; i < 8; ++i) cw[i] = 0;

@@ -109,6 +109,10 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
 template <int W = 4>
 __device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
                                              uint32_t yi, uint32_t cnt, uint32_t A) {
+  if (W > 1 && cnt == 1) {            // one new entry (a client-set append): one load each
+    const uint2 x = xa[xi], y = ya[yi];
+    return x.x == y.x && x.y != y.y;
+  }
   for (uint32_t i = 0; i < cnt; i += W) {
     uint2 x[W], y[W];
 #pragma unroll
@@ -370,7 +374,7 @@ constexpr int wave_lds_words() {
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
+  return wave_lds_words<N, SPEC>() * sizeof(uint32_t);
 }
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
@@ -401,10 +405,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
-  // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters and leader rows
-  unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
-  if (lane < 32) pw[lane] = S.client_pw[lane];
-  uint32_t* cells = smem + PW_WORDS;
+  // the wave's cells, counters, leader rows and per-lane words
+  uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
@@ -484,7 +486,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           const uint4 d = philox(g, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
           ++cnt;
           ++ccount;
-          cnext = client_next_tick(cnext, d.w, pw, S.client_top, S.client_period, S.client_burst);
+          cnext = client_next_tick(cnext, d.w, S);
         }
         if (active && k0 == 0) {
           lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
@@ -593,7 +595,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             injv = d.z;
           }
           ccount += 1;
-          cnext = client_next_tick(t, d.w, pw, S.client_top, S.client_period, S.client_burst);
+          cnext = client_next_tick(t, d.w, S);
         }
       }
 
@@ -962,7 +964,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             bool part = false;
             uint32_t sides = 0;
             if (!LITE && S.part_ppm) {
-              const uint4 pw = philox(sg, P_PART << 8, t / S.part_epoch, 0, S.key0, S.key1);
+              const uint4 pw = philox(sg, P_PART << 8, udiv(S.div_epoch, t), 0, S.key0, S.key1);
               part = ppm(pw.x) < S.part_ppm;
               sides = pw.y;
             }
