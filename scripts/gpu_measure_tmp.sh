@@ -11,3 +11,7 @@ timeout -k 10 200 python -u scripts/wavelog_probe.py raft-simulation_amd/build/l
 cat gpurun_out/wl_c3.txt
 timeout -k 10 200 python -u scripts/wavelog_probe.py raft-simulation_amd/build/libraftsim_wavelog.so 131072 c3_spec 4 > gpurun_out/wl_c3s.txt 2>&1 || { echo "wl c3s failed"; tail gpurun_out/wl_c3s.txt; exit 1; }
 cat gpurun_out/wl_c3s.txt
+cd $GRAFT_REPO_ROOT
+hipcc --offload-arch=gfx950 -O3 -o /tmp/launch_probe scripts/launch_probe.hip > /dev/null 2>&1 || { echo "probe build failed"; exit 1; }
+timeout -k 10 60 /tmp/launch_probe > gpurun_out/launch_probe.txt 2>&1 || { echo "probe failed"; exit 1; }
+cat gpurun_out/launch_probe.txt

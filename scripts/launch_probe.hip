@@ -19,10 +19,14 @@ __global__ void __launch_bounds__(256) dirty_kernel(uint32_t* p, uint32_t v) {
   for (int i = 0; i < 4; ++i) b[i] = make_uint4(v, v + i, c, 0);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) dirty_nt_kernel(uint32_t* p, uint32_t v) {
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-  uint4* b = reinterpret_cast<uint4*>(p + (size_t)c * 160 + 8);
-  for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(make_uint4(v, v + i, c, 0), b + i);
+  u32x4* b = reinterpret_cast<u32x4*>(p + (size_t)c * 160 + 8);
+  for (int i = 0; i < 4; ++i) {
+    const u32x4 x = {v, v + i, c, 0u};
+    __builtin_nontemporal_store(x, b + i);
+  }
 }
 
 // the load shape of the steady kernel: 31 x 16 B per lane from its block, summed
