@@ -29,6 +29,7 @@ enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min violation tick
 constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
+constexpr int PW_WORDS = 64;    // 32 x u64 client-gap powers at the start of the wave's LDS
 static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
 // Waves flush their counters into one of CTR_COPIES copies of the counter block (wave index mod
 // CTR_COPIES): thousands of waves ending together otherwise serialise on the same few words of
@@ -177,7 +178,8 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
 // are 0 and never fire). The accumulator starts at 2^32 and every power is below 2^32 when
 // client_ppm > 0, so after its first step it fits 32 bits and (acc * pw) >> 32 is one
 // v_mul_hi_u32 instead of a 64x64-bit product.
-// pw is the kernel argument's table: the loop index is uniform, so each power is a scalar load.
+// pw: the wave's LDS copy of the table (scalar loads from the kernel argument's copy measured
+// slower: each step waits on its own load).
 __device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
   // client_ppm == 0 (top == 32; reachable only through a host-written client cursor): every
   // power is 2^32, so the search takes every step
@@ -209,11 +211,12 @@ __device__ inline uint32_t on_tick(uint64_t j, uint32_t P, const DivU32& B) {
   return t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
 }
 // The next injection after the one at tick t (an on-tick), drawing gap word w.
-__device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const DevSim& S) {
+__device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const DevSim& S,
+                                            const unsigned long long* pw) {
   const uint32_t P = S.client_period;
   const uint32_t q = P ? udiv(S.div_period, t) : 0u;
   const uint64_t j = P ? (uint64_t)q * S.div_burst.d + (t - q * P) : t;
-  return on_tick(j + 1 + client_gap(w, S.client_pw, S.client_top), P, S.div_burst);
+  return on_tick(j + 1 + client_gap(w, pw, S.client_top), P, S.div_burst);
 }
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;

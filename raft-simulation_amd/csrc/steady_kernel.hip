@@ -32,7 +32,6 @@
 namespace rs {
 
 constexpr int LANE_WG = 256;                 // four waves, 64 clusters each
-constexpr int LANE_WAVES = LANE_WG / 64;
 
 // v = vals[k] for a runtime k < N, as masks (a select chain over an array is turned back into an
 // indexed load from memory by the compiler; this keeps the array in registers)
@@ -49,10 +48,12 @@ __device__ __forceinline__ uint32_t msel(bool a, uint32_t x, uint32_t y) {
   return (x & m) | (y & ~m);
 }
 
-// Dynamic LDS of a steady workgroup: one tick_wave LDS block per wave for the catch-up.
+// Dynamic LDS of a steady workgroup: one tick_wave LDS block for the catch-up, which the
+// workgroup's first wave runs alone (hand-overs are rare where the steady path is taken, and four
+// blocks' LDS measured +0.8 us on every dispatch's launch).
 template <int N>
 constexpr size_t steady_lds_bytes() {
-  return LANE_WAVES * block_lds_bytes<N, false>();
+  return block_lds_bytes<N, false>();
 }
 
 template <int N>
@@ -73,9 +74,11 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // the previous steady launch's bail count (complete: that launch has ended) to the host, which
     // picks the next launches' path from it (speed only); that word is this launch's successor's
+    // (host memory is written only when there is something to report: the host zeroes its copy
+    // when it acts on it, and a store there holds the launch's end for a bus round trip)
     const uint32_t prev = *S.nbail_zero;
-    if (S.bail_report) *S.bail_report = prev;
-    *S.nbail_zero = 0;
+    if (S.bail_report && prev) *S.bail_report = prev;
+    if (prev) *S.nbail_zero = 0;
   }
   if (threadIdx.x < 4) sctr[threadIdx.x] = 0;
   if (threadIdx.x == 0) nbl = 0;
@@ -362,11 +365,12 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       // The whole heartbeat round in this trip when nothing else can happen before its last
       // response: every follower takes the append-entries at t + d (no follower deadline before
       // it; the handler's checks pass), the followers' re-armed deadlines (>= t + d + el_base) and
-      // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the round
-      // ends before the launch does (and no older response is still queued). The responses then
-      // run as a drain (which stops at one outside the model; the next trip decides it). A
-      // deferred deadline counts with its lower bound here (a round not taken is run tick by tick).
-      round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > 2 * d + F;
+      // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the
+      // append-entries come before the launch ends (and no older response is still queued). The
+      // responses then run in slot order up to the launch end (the rest stay queued) and stop at
+      // one outside the model (the next trip decides it). A deferred deadline counts with its
+      // lower bound here (a round not taken is run tick by tick).
+      round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > d;
 #pragma unroll
       for (int j = 0; j < F; ++j)
         round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
@@ -430,8 +434,9 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       append_entries(t + d, (1u << F) - 1);
       bool go = true;
 #pragma unroll
-      for (int j = 0; j < F; ++j)
-        go = go && response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
+      for (int j = 0; j < F; ++j)     // (a round cut by the launch end leaves the rest queued)
+        go = go && t + 2 * d + j < tend &&
+             response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
       if (!rmask) resA = INF;
       // A round that ran every response leaves the cluster in its fixed point: every follower
       // took the append-entries (its flags, votes, term and commit are what another one sets
@@ -465,18 +470,23 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         nae += F * R;
         nar += F * R;
       }
-    } else if (fae) {
-      append_entries(t, fae);
-    } else if (lres) {
-      // from t one response per tick, heads in sender order, while nothing else in the cluster
-      // is due (the followers' next events and the launch end; the leader's own deadline moves
-      // past each); the first one at t was decided above. A response outside the model ends the
-      // run and the next trip decides it.
+    } else if (fae || lres) {
+      // fae: the append-entries at t, then their responses from t + d in the same trip unless
+      // the leader's heartbeat falls due before them. The responses run one per tick, heads in
+      // sender order, while nothing else in the cluster is due (the followers' next events and
+      // the launch end; the leader's own deadline moves past each); lres: the first one at t
+      // was decided above. A response outside the model ends the run and the next trip
+      // decides it.
+      uint32_t tau0 = t;
+      if (fae) {
+        append_entries(t, fae);
+        tau0 = Ldl >= t + d ? t + d : tend;
+      }
       uint32_t E = tend;
 #pragma unroll
       for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
-      E = max(E, t + 1);
-      for (uint32_t tau = t; rmask && tau < E; ++tau) {
+      if (lres) E = max(E, t + 1);
+      for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
         const int h2 = __builtin_ctz(rmask);
         bool ok = true;
 #pragma unroll
@@ -625,14 +635,12 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   }
   // ---------------------------------------------------------------- catch-up
   // The bailed clusters, each from the tick it stopped before to the launch's end, through the
-  // general tick body: wave w of the workgroup takes wave slots w, w + 4, ... of the list.
+  // general tick body: the workgroup's first wave takes the list's wave slots in turn.
   const uint32_t nb = nbl;
-  if (nb == 0) return;                                        // workgroup-uniform
+  if (nb == 0 || threadIdx.x >= 64) return;                   // wave-uniform
   if (threadIdx.x == 0) atomicAdd(S.nbail, nb);
-  const uint32_t wv = threadIdx.x >> 6;
-  tick_wave<N, false, false, true, true>(
-      S, t0, nt, dsm + wv * (block_lds_bytes<N, false>() / sizeof(uint32_t)), (int)lane, wv,
-      LANE_WAVES, bl_c, nb, bl_t, blockIdx.x * LANE_WAVES + wv);
+  tick_wave<N, false, false, true, true>(S, t0, nt, dsm, (int)lane, 0, 1, bl_c, nb, bl_t,
+                                         blockIdx.x);
 }
 
 hipError_t configure_steady() {

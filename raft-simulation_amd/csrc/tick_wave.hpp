@@ -374,7 +374,7 @@ constexpr int wave_lds_words() {
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return wave_lds_words<N, SPEC>() * sizeof(uint32_t);
+  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
 }
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
@@ -405,8 +405,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
-  // the wave's cells, counters, leader rows and per-lane words
-  uint32_t* cells = smem;
+  // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters, leader rows and
+  // per-lane words
+  unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
+  if (lane < 32) pw[lane] = S.client_pw[lane];
+  uint32_t* cells = smem + PW_WORDS;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
@@ -486,7 +489,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           const uint4 d = philox(g, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
           ++cnt;
           ++ccount;
-          cnext = client_next_tick(cnext, d.w, S);
+          cnext = client_next_tick(cnext, d.w, S, pw);
         }
         if (active && k0 == 0) {
           lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
@@ -595,7 +598,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             injv = d.z;
           }
           ccount += 1;
-          cnext = client_next_tick(t, d.w, S);
+          cnext = client_next_tick(t, d.w, S, pw);
         }
       }
 
