@@ -45,6 +45,11 @@ struct Shard {
   uint64_t ticks_run;   // ticks simulated by this handle (node_ticks counts these)
   hipStream_t stream;
   hipEvent_t ev_start, ev_stop;
+  // Start/stop events in a launch's dispatch packet time the kernel alone, but measured 8.2 against
+  // 2.5 us per back-to-back launch of an empty kernel on MI355X (scripts/launch_probe.hip): by
+  // default only the first launch after a sync carries them (the kernel time reported is that
+  // launch's), RAFTSIM_LAUNCH_EVENTS=1 times every launch (diagnostic).
+  bool launch_events;
   std::vector<hipEvent_t> kev;   // per tick-kernel launch of a step: start, stop
   DevSim d;
   std::vector<void*> allocs;
@@ -229,6 +234,10 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
 #endif
   s->steady_ok = d.lite && s->N <= 5 && !d.TC && !(cfg->variant_flags & RAFT_VARIANT_SPEC);
   s->resort_every = d.lite ? RESORT_EVERY_LITE : RESORT_EVERY;
+  {
+    const char* le = getenv("RAFTSIM_LAUNCH_EVENTS");
+    s->launch_events = le && !strcmp(le, "1");
+  }
   if (s->steady_ok && (rc = dalloc(s, &s->nbail2, 2))) {
     sh_destroy(s);
     return rc;
@@ -338,7 +347,8 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       s->keys_written = s->resort_ctr % s->resort_every == 0;   // the next launch rebuilds
       no_keys = !s->keys_written;
     }
-    while (s->kev.size() < 2 * (size_t)(launches + 1)) {
+    const bool timed = s->launch_events || launches == 0;
+    while (timed && s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
       s->kev.push_back(e);
@@ -356,8 +366,9 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     DevSim D = s->d;
     if (no_perm) D.perm = nullptr;
     if (no_keys) D.shist = nullptr;
-    HIP_OK(rs::launch_tick(D, t0, nt, s->stream, s->kev[2 * launches], s->kev[2 * launches + 1],
-                           steady));
+    HIP_OK(rs::launch_tick(D, t0, nt, s->stream,
+                           timed ? s->kev[2 * launches] : nullptr,
+                           timed ? s->kev[2 * launches + 1] : nullptr, steady));
     done += nt;
     s->tick += nt;
     s->ticks_run += nt;
@@ -381,12 +392,13 @@ static int sh_sync(Shard* s) {
   HIP_OK(hipEventSynchronize(s->ev_stop));
   float ms = 0, kms = 0;
   HIP_OK(hipEventElapsedTime(&ms, s->ev_start, s->ev_stop));
-  for (uint32_t i = 0; i < launches; ++i) {
+  const uint32_t timed = s->launch_events ? launches : std::min(launches, 1u);
+  for (uint32_t i = 0; i < timed; ++i) {
     float one = 0;
     HIP_OK(hipEventElapsedTime(&one, s->kev[2 * i], s->kev[2 * i + 1]));
     kms += one;
   }
-  s->last_ms = launches ? kms / launches : 0.0;   // tick kernel alone
+  s->last_ms = timed ? kms / timed : 0.0;         // per tick-kernel launch
   s->last_step_ms = ms;                           // + the schedule's key and sort kernels
   s->last_launches = launches;
   return 0;

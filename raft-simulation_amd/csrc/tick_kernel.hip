@@ -300,8 +300,9 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
   out[ci] = h;
 }
 
-// The tick kernel's own start/stop timestamps go into ev0/ev1 through its dispatch packet
-// (hipExtLaunchKernelGGL): no marker packets between launches (each cost ~5.7 us of idle GPU).
+// The tick kernel's own start/stop timestamps go into ev0/ev1 (null: none) through its dispatch
+// packet (hipExtLaunchKernelGGL: no marker packets between launches, each of which cost ~5.7 us of
+// idle GPU); the host times one launch per sync that way (raftsim.hip, launch_events).
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0, hipEvent_t ev1);
 

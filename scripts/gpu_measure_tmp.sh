@@ -15,3 +15,5 @@ cd $GRAFT_REPO_ROOT
 hipcc --offload-arch=gfx950 -O3 -o /tmp/launch_probe scripts/launch_probe.hip > /dev/null 2>&1 || { echo "probe build failed"; exit 1; }
 timeout -k 10 60 /tmp/launch_probe > gpurun_out/launch_probe.txt 2>&1 || { echo "probe failed"; exit 1; }
 cat gpurun_out/launch_probe.txt
+timeout -k 10 120 python scripts/dispatch_probe.py raft-simulation_amd/build/libraftsim.so raft-simulation_amd/build/libraftsim_loadonly.so > gpurun_out/dispatch_probe.txt 2>&1 || { echo "dprobe failed"; tail gpurun_out/dispatch_probe.txt; exit 1; }
+cat gpurun_out/dispatch_probe.txt

@@ -4,6 +4,7 @@
 // steady kernel's write-back shape), with plain and with write-through (nontemporal) stores.
 // Build: hipcc --offload-arch=gfx950 -O3 -o /tmp/launch_probe scripts/launch_probe.hip
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdio.h>
 #include <stdint.h>
 
@@ -27,6 +28,12 @@ __global__ void __launch_bounds__(256) dirty_nt_kernel(uint32_t* p, uint32_t v) 
     const u32x4 x = {v, v + i, c, 0u};
     __builtin_nontemporal_store(x, b + i);
   }
+}
+
+// empty, but each workgroup's first 5 threads add to 64 copies of a counter block at the end
+__global__ void __launch_bounds__(256) atomics_kernel(unsigned long long* ctr) {
+  __syncthreads();
+  if (threadIdx.x < 5) atomicAdd(&ctr[(blockIdx.x % 64) * 32 + threadIdx.x], 1ull);
 }
 
 // the load shape of the steady kernel: 31 x 16 B per lane from its block, summed
@@ -70,6 +77,19 @@ int main() {
     }, reps);
     printf("empty kernel, %u x 256 threads, %d B dynamic LDS: %.2f us per launch\n", blocks, lds, us);
   }
+  {
+    hipEvent_t e0, e1;
+    hipEventCreateWithFlags(&e0, hipEventDisableSystemFence);
+    hipEventCreateWithFlags(&e1, hipEventDisableSystemFence);
+    printf("empty kernel with start/stop events in its packet: %.2f us per launch\n", time_launches([&] {
+      hipExtLaunchKernelGGL(empty_kernel, dim3(blocks), dim3(256), 40960, 0, e0, e1, 0, p);
+    }, reps));
+  }
+  unsigned long long* ctr = nullptr;
+  hipMalloc(&ctr, 64 * 32 * 8);
+  printf("empty kernel + 5 atomics per workgroup: %.2f us per launch\n", time_launches([&] {
+    hipLaunchKernelGGL(atomics_kernel, dim3(blocks), dim3(256), 0, 0, ctr);
+  }, reps));
   uint32_t v = 1;
   printf("dirty plain: %.2f us per launch\n", time_launches([&] {
     hipLaunchKernelGGL(dirty_kernel, dim3(blocks), dim3(256), 0, 0, p, v++);
