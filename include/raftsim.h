@@ -240,12 +240,12 @@ int raft_sim_read_counters(raft_sim_t* sim, raft_counters_t* out);
 /* Per-cluster FNV-1a-64 digest of the canonical state (SIM_SPEC §6). */
 int raft_sim_digest(raft_sim_t* sim, uint32_t c0, uint32_t nc, uint64_t* out);
 
-/* Device time of a tick-kernel launch of the last raft_sim_step (or of the raft_sim_step_async
- * calls since the previous sync, once raft_sim_sync returned) alone, and the launch count; for
- * bench.py's roofline. An event pair in the dispatch packet of the first launch after a sync
- * times it (such a pair costs ~6 us per launch on MI355X, so the other launches carry none); with
- * RAFTSIM_LAUNCH_EVENTS=1 in the environment at create every launch is timed and the average
- * returned. */
+/* Average device time of the tick-kernel launches of the last raft_sim_step (or of the
+ * raft_sim_step_async calls since the previous sync, once raft_sim_sync returned) alone, and the
+ * launch count; for bench.py's roofline. An event pair in a launch's dispatch packet times it:
+ * every general-kernel launch, and of the steady-path launches (~0.025 ms at config 2) only one
+ * that comes first after a sync, since such a pair costs ~6 us per launch on MI355X; with
+ * RAFTSIM_LAUNCH_EVENTS=1 in the environment at create every launch is timed. */
 int raft_sim_last_step_timing(raft_sim_t* sim, double* avg_kernel_ms, uint32_t* launches);
 
 /* Device time of everything the last raft_sim_step (or every raft_sim_step_async since the

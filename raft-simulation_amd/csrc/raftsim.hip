@@ -46,10 +46,13 @@ struct Shard {
   hipStream_t stream;
   hipEvent_t ev_start, ev_stop;
   // Start/stop events in a launch's dispatch packet time the kernel alone, but measured 8.2 against
-  // 2.5 us per back-to-back launch of an empty kernel on MI355X (scripts/launch_probe.hip): by
-  // default only the first launch after a sync carries them (the kernel time reported is that
-  // launch's), RAFTSIM_LAUNCH_EVENTS=1 times every launch (diagnostic).
+  // 2.5 us per back-to-back launch of an empty kernel on MI355X (scripts/launch_probe.hip): a
+  // steady-path launch (~0.025 ms at C2) carries them only when it is the first after a sync
+  // (the kernel time reported is that launch's); general-kernel launches (milliseconds, and their
+  // cost changes over a run as logs grow and nodes halt) are all timed. RAFTSIM_LAUNCH_EVENTS=1
+  // times every launch (diagnostic).
   bool launch_events;
+  std::vector<uint8_t> ktimed;   // per launch since the last sync: carries an event pair
   std::vector<hipEvent_t> kev;   // per tick-kernel launch of a step: start, stop
   DevSim d;
   std::vector<void*> allocs;
@@ -347,7 +350,9 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
       s->keys_written = s->resort_ctr % s->resort_every == 0;   // the next launch rebuilds
       no_keys = !s->keys_written;
     }
-    const bool timed = s->launch_events || launches == 0;
+    const bool timed = s->launch_events || launches == 0 || !steady;
+    if (s->ktimed.size() < launches + 1) s->ktimed.resize(launches + 1);
+    s->ktimed[launches] = timed;
     while (timed && s->kev.size() < 2 * (size_t)(launches + 1)) {
       hipEvent_t e;   // timing only: no system-scope fence (cache writeback) per launch
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -392,11 +397,13 @@ static int sh_sync(Shard* s) {
   HIP_OK(hipEventSynchronize(s->ev_stop));
   float ms = 0, kms = 0;
   HIP_OK(hipEventElapsedTime(&ms, s->ev_start, s->ev_stop));
-  const uint32_t timed = s->launch_events ? launches : std::min(launches, 1u);
-  for (uint32_t i = 0; i < timed; ++i) {
+  uint32_t timed = 0;
+  for (uint32_t i = 0; i < launches; ++i) {
+    if (!s->ktimed[i]) continue;
     float one = 0;
     HIP_OK(hipEventElapsedTime(&one, s->kev[2 * i], s->kev[2 * i + 1]));
     kms += one;
+    ++timed;
   }
   s->last_ms = timed ? kms / timed : 0.0;         // per tick-kernel launch
   s->last_step_ms = ms;                           // + the schedule's key and sort kernels

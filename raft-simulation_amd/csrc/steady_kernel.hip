@@ -646,6 +646,14 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   // The bailed clusters, each from the tick it stopped before to the launch's end, through the
   // general tick body: the workgroup's first wave takes the list's wave slots in turn.
   const uint32_t nb = nbl;
+#ifdef RS_WAVELOG   // the workgroup's end: its stores drained (the barrier's release) and counted
+  if (threadIdx.x == 0 && S.wavelog) {
+    const uint64_t wl_done = wall_clock64();
+    uint32_t* rec = S.wavelog + (size_t)(blockIdx.x * 4) * 32;
+    rec[17] = (uint32_t)wl_done;
+    rec[18] = (uint32_t)(wl_done >> 32);
+  }
+#endif
   if (nb == 0 || threadIdx.x >= 64) return;                   // wave-uniform
   if (threadIdx.x == 0) atomicAdd(S.nbail, nb);
   tick_wave<N, false, false, true, true>(S, t0, nt, dsm, (int)lane, 0, 1, bl_c, nb, bl_t,

@@ -37,6 +37,11 @@ print("lanes on    p0/10/50/90/99/100:", q(a[:, 7]))
 print("events/lane min p0/10/50/90/99/100:", q(a[:, 10]))
 print("events/lane max p0/10/50/90/99/100:", q(a[:, 11]))
 print("us per trip p0/10/50/90/99/100:", q((a[:, 9] - a[:, 8]) / 100.0 / np.maximum(a[:, 4], 1)))
+done = a[:, 17] | (a[:, 18] << 32)
+done = done[done != 0]
+if len(done):
+    print(f"workgroup done (stores drained, counters added) us after the first start: "
+          f"p50 {np.percentile((done - t0) / 100.0, 50):.1f} max {(done.max() - t0) / 100.0:.1f}")
 hw, xcc = a[:, 5], a[:, 6]
 simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) & 7
 key = xcc * 10000 + se * 1000 + sh * 100 + cu * 4 + simd
