@@ -295,6 +295,9 @@ __device__ __forceinline__ size_t qstride(const DevSim& S, int which) {
   return which ? 8 : (size_t)S.NN * 8;
 }
 
+// slots of padding after the last node's arena: the chunked arena loops (tick_wave.hpp) may read
+// up to 7 slots past a run's end
+constexpr uint32_t ARENA_PAD_SLOTS = 16;
 __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
   return reinterpret_cast<uint2*>(S.arena) + (size_t)gi * S.A;
 }

@@ -216,7 +216,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   d.HB = rs::hot_block_words(s->N);
   if ((rc = dalloc(s, &d.hot, (size_t)s->C * d.HB)) ||
       (rc = dalloc(s, &d.qbuf, NN * 2 * s->Q * 8)) ||
-      (rc = dalloc(s, &d.arena, NN * (size_t)s->A * 2)) ||
+      (rc = dalloc(s, &d.arena, (NN * (size_t)s->A + rs::ARENA_PAD_SLOTS) * 2)) ||
       (rc = dalloc(s, &d.ctr, (size_t)rs::CTR_COPIES * rs::CTR_STRIDE)) || (rc = dalloc(s, &s->client_pw, 32)) ||
       (rc = dalloc(s, &d.ccount, NN)) ||
       (rc = dalloc(s, &d.stream, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1))) ||
@@ -275,7 +275,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
       (e = hipEventCreate(&s->ev_stop)) != hipSuccess ||
       (e = hipMemsetAsync(d.hot, 0, (size_t)s->C * d.HB * 4, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.qbuf, 0, NN * 2 * s->Q * 32, s->stream)) != hipSuccess ||
-      (e = hipMemsetAsync(d.arena, 0, NN * (size_t)s->A * 8, s->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(d.arena, 0, (NN * (size_t)s->A + rs::ARENA_PAD_SLOTS) * 8, s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.stream, 0, NN * std::max<uint32_t>(cfg->commit_stream_cap, 1) * 4,
                           s->stream)) != hipSuccess ||
       (e = hipMemsetAsync(d.tr, 0, NN * std::max<uint32_t>(d.TC, 1) * 128, s->stream)) != hipSuccess ||

@@ -11,9 +11,9 @@ namespace rs {
 // and a multi-wave workgroup holds its CU slot and LDS until its slowest wave ends; measured:
 // 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound. The
 // compiler is asked for 4 waves per SIMD (<= 128 VGPRs) where it meets that without spilling:
-// N <= 5, and the faithful kernels up to N = 8 (unasked it took 129 for some of them).
+// N <= 5, and the faithful kernels up to N = 6 (N = 7, 8 would spill).
 template <int N, bool TRACE, bool SPEC, bool LITE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(!TRACE && (N <= 5 || (!SPEC && N <= 8)) ? 4 : 1, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(!TRACE && (N <= 5 || (!SPEC && N <= 6)) ? 4 : 1, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   tick_wave<N, TRACE, SPEC, LITE>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x, gridDim.x, S.perm,

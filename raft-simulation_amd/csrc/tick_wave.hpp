@@ -33,35 +33,35 @@ __device__ __forceinline__ void cell_put(uint32_t* cl, uint4 a, uint4 b) {
   cl[4] = b.z;
 }
 
-// P2 fault draws for one emitted message whose words are already in cell `cl`: the delivery pack
-// (copy delays and count) goes to the cell's last word and the receiver's bit into sentmask.
-template <int N, bool LITE>
-__device__ __forceinline__ void transmit(const DevSim& S, uint32_t g, uint32_t t, uint32_t id,
-                                         uint32_t p, bool part, uint32_t sides, uint32_t* cl,
-                                         uint32_t& sentmask, uint32_t* lctr) {
-  // RAFT_CTR_SENT is counted by the caller (once per emission: 1 or N - 1)
-  if (part && (((sides >> id) ^ (sides >> p)) & 1)) {
+// P2 fault draws for one network message from node `src` to node `id` emitted at tick t (keyed by
+// cluster, sender, tick and receiver). Returns the delivery pack: copy 0's delay in bits 0-7, copy
+// 1's in bits 8-15, the copy count (0: lost) in bits 16-17. (Made by the receivers' lanes instead
+// -- a broadcast's draws in parallel -- C3 was 3 % slower: a leader's N - 1 responses then cost
+// its lane N - 1 draws in a row.)
+template <bool LITE>
+__device__ __forceinline__ uint32_t deliver_pack(const DevSim& S, uint32_t g, uint32_t t,
+                                                 uint32_t src, uint32_t id, uint32_t pstate,
+                                                 uint32_t* lctr) {
+  if (LITE || (!S.drop_ppm && !S.dup_ppm && !S.part_ppm && S.dmin == S.dmax))
+    return S.dmin | 1u << 16;
+  // pstate: the cluster's partition draw of this epoch (bit 0: partitioned, bit i: node i's side)
+  if ((pstate & 1) && (((pstate >> id) ^ (pstate >> src)) & 1)) {
     lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
-    return;
+    return 0;
   }
-  uint32_t pack;
-  if (LITE || (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax)) {
-    pack = S.dmin | 1u << 16;
-  } else {
-    const uint4 w = philox(g, id | P_NET << 8, t, p, S.key0, S.key1);
-    if (ppm(w.x) < S.drop_ppm) {
-      lctr_add(lctr, RAFT_CTR_DROPPED, 1);
-      return;
-    }
-    const uint32_t span = S.dmax - S.dmin + 1;
-    pack = (S.dmin + __umulhi(w.z, span)) | 1u << 16;
-    if (ppm(w.y) < S.dup_ppm) {
-      lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
-      pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
-    }
+  if (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax) return S.dmin | 1u << 16;
+  const uint4 w = philox(g, src | P_NET << 8, t, id, S.key0, S.key1);
+  if (ppm(w.x) < S.drop_ppm) {
+    lctr_add(lctr, RAFT_CTR_DROPPED, 1);
+    return 0;
   }
-  cl[CELLW - 1] = pack;
-  sentmask |= 1u << p;
+  const uint32_t span = S.dmax - S.dmin + 1;
+  uint32_t pack = (S.dmin + __umulhi(w.z, span)) | 1u << 16;
+  if (ppm(w.y) < S.dup_ppm) {
+    lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
+    pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
+  }
+  return pack;
 }
 
 // A node's leader-state words next_index / match_index (peer p = id - 1). In HBM they are fields
@@ -101,67 +101,71 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   for (int i = 0; i < 8; ++i) rec[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
+// Arena runs. A node's arena is A slots; a run of consecutive log positions starts at some slot
+// and wraps at A. The loops below take a run W (or B) slots at a time with one address per
+// run and immediate-offset loads -- a chunk ends at the run's end or at either arena's wrap point,
+// whichever is first -- so a position costs a few VALU instead of the ~16 of a per-slot wrap and
+// 64-bit address. A chunk's loads may read up to W - 1 slots past its end: inside the next node's
+// arena, or the ARENA_PAD_SLOTS of padding after the last one (raftsim.hip); those lanes of the
+// chunk are masked.
+
 // Log Matching over cnt consecutive positions of two logs whose first slots are xi in arena xa
-// and yi in arena ya (slots wrap at A): is there a position with the same term and a different
-// value? Four positions per trip with their eight loads in flight together (a 2000-entry
-// AppendEntries is checked against every peer: one memory round trip per entry was most of C4's
-// time); every slot read is inside the arena, the comparisons past cnt are masked.
-template <int W = 4>
+// and yi in arena ya: is there a position with the same term and a different value?
+template <int W = 8>
 __device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
                                              uint32_t yi, uint32_t cnt, uint32_t A) {
-  if (W > 1 && cnt == 1) {            // one new entry (a client-set append): one load each
-    const uint2 x = xa[xi], y = ya[yi];
-    return x.x == y.x && x.y != y.y;
-  }
-  for (uint32_t i = 0; i < cnt; i += W) {
+  while (cnt) {
+    const uint32_t c = min(min(cnt, (uint32_t)W), min(A - xi, A - yi));
+    const uint2* xp = xa + xi;
+    const uint2* yp = ya + yi;
     uint2 x[W], y[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-      x[j] = xa[xi];
-      y[j] = ya[yi];
-      xi = xi + 1 == A ? 0 : xi + 1;
-      yi = yi + 1 == A ? 0 : yi + 1;
+      x[j] = xp[j];
+      y[j] = yp[j];
     }
-    bool c = false;
+    bool hit = false;
 #pragma unroll
-    for (int j = 0; j < W; ++j) c |= i + j < cnt && x[j].x == y[j].x && x[j].y != y[j].y;
-    if (c) return true;
+    for (int j = 0; j < W; ++j) hit |= (uint32_t)j < c && x[j].x == y[j].x && x[j].y != y[j].y;
+    if (hit) return true;
+    cnt -= c;
+    xi += c;
+    yi += c;
+    xi = xi == A ? 0 : xi;
+    yi = yi == A ? 0 : yi;
   }
   return false;
 }
 
-// Copy `cnt` arena entries from slot si of `src` to slot di of `dst` (slots wrap at A), eight per
-// batch: a batch's loads are all issued before its stores, so a long copy pays one memory round
-// trip per eight entries rather than one per entry. Ascending order with every load of a batch
-// ahead of its stores keeps an overlapping relocation (dst ahead of src by d < A) exact: a slot
-// is only overwritten after it has been read, as in the oracle's element-by-element copy.
-template <uint32_t B = 4>
+// Copy `cnt` arena entries from slot si of `src` to slot di of `dst`, in ascending order with every
+// load of a B-slot chunk ahead of its stores. That reproduces the oracle's element-by-element copy
+// also for a relocation inside one arena (dst = the frontier, src = the old base): the distance
+// d = frontier - base satisfies cnt <= d < A (a log never exceeds L <= A / 2 positions past its
+// base), so a slot the copy overwrites is one it read at an earlier position (or in the same
+// chunk, before the chunk's stores).
+template <uint32_t B = 8>
 __device__ __forceinline__ void arena_copy(uint2* dst, uint32_t di, const uint2* src, uint32_t si,
                                            uint32_t cnt, uint32_t A) {
-  uint32_t i = 0;
-  if (A >= B) {
-    for (; i + B <= cnt; i += B) {
+  while (cnt) {
+    if (cnt >= B && si + B <= A && di + B <= A) {
       uint2 v[B];
+      const uint2* sp = src + si;
+      uint2* dp = dst + di;
 #pragma unroll
-      for (int j = 0; j < (int)B; ++j) {
-        const uint32_t s = si + j;
-        v[j] = src[s >= A ? s - A : s];
-      }
+      for (int j = 0; j < (int)B; ++j) v[j] = sp[j];
 #pragma unroll
-      for (int j = 0; j < (int)B; ++j) {
-        const uint32_t d = di + j;
-        dst[d >= A ? d - A : d] = v[j];
-      }
+      for (int j = 0; j < (int)B; ++j) dp[j] = v[j];
       si += B;
-      si = si >= A ? si - A : si;
       di += B;
-      di = di >= A ? di - A : di;
+      cnt -= B;
+    } else {
+      dst[di] = src[si];
+      ++si;
+      ++di;
+      --cnt;
     }
-  }
-  for (; i < cnt; ++i) {
-    dst[di] = src[si];
-    si = si + 1 == A ? 0 : si + 1;
-    di = di + 1 == A ? 0 : di + 1;
+    si = si == A ? 0 : si;
+    di = di == A ? 0 : di;
   }
 }
 
@@ -240,18 +244,47 @@ __device__ __forceinline__ void spec_handle(
       if (!consistent) break;
       // first conflict in [b, min(len, b + pcnt)); the payload is read from the sender's arena,
       // an entry its pre-tick frontier has overwritten reading (0, 0)
+      // (payload position i reads (0, 0) iff the sender's pre-tick frontier passed mpoff + i + A:
+      // a prefix i < E of the payload; evictions are counted over the positions compared)
       const uint64_t sf0 = fr[bl + (int)src - 1];
       const uint2* sa = arena_of(S, sgi - k + src - 1);
       const uint32_t hi = n.len < mb + pcnt ? n.len : mb + pcnt;
-      uint32_t kk = mb, evc = 0;
-      for (; kk < hi; ++kk) {
-        const uint32_t i = kk - mb;
-        uint32_t pt = 0;
-        if (sf0 > (uint64_t)mpoff + i + A) ++evc;
-        else pt = sa[(mpoff + i) % A].x;
-        if (sar[(n.base + kk) % A].x != pt) break;
+      const int64_t ev64 = (int64_t)sf0 - (int64_t)mpoff - (int64_t)A;
+      const uint32_t E = ev64 <= 0 ? 0u : (ev64 >= (int64_t)pcnt ? pcnt : (uint32_t)ev64);
+      uint32_t kk = mb;
+      if (kk < hi) {
+        uint32_t yi = (n.base + kk) % A, xi = mpoff % A, rem = hi - kk;
+        constexpr int W = 8;
+        while (rem) {
+          const uint32_t c = min(min(rem, (uint32_t)W), min(A - xi, A - yi));
+          const uint2* xp = sa + xi;
+          const uint2* yp = sar + yi;
+          uint32_t xt[W], yt[W];
+#pragma unroll
+          for (int j = 0; j < W; ++j) {
+            xt[j] = xp[j].x;
+            yt[j] = yp[j].x;
+          }
+          const uint32_t i0 = kk - mb;
+          uint32_t mism = 0;
+#pragma unroll
+          for (int j = 0; j < W; ++j)
+            mism |= (uint32_t)((uint32_t)j < c && yt[j] != (i0 + j < E ? 0u : xt[j])) << j;
+          if (mism) {
+            kk += __builtin_ctz(mism);
+            break;
+          }
+          kk += c;
+          rem -= c;
+          xi += c;
+          yi += c;
+          xi = xi == A ? 0 : xi;
+          yi = yi == A ? 0 : yi;
+        }
       }
-      lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evc);
+      // positions compared: [mb, kk] on a mismatch at kk (< hi), else [mb, hi)
+      const uint32_t ncmp = kk < hi ? kk - mb + 1 : hi > mb ? hi - mb : 0u;
+      lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, ncmp < E ? ncmp : E);
       const uint32_t mc = mb + pcnt - kk;
       if (mc) {                               // truncate at kk, append payload [kk - b, pcnt)
         pkind = PLAN_PAYLOAD; psrc = src; ppoff = mpoff + (kk - mb); ppcnt = mc;
@@ -365,12 +398,14 @@ template <int N>
 constexpr bool nm_lds() { return N <= 5; }
 // TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key);
 // DPEND_WORDS: per lane, 1 while its node's deadline is a deferred re-arm's lower bound
+// PART_WORDS: per cluster slot, the partition epoch last drawn and its draw (deliver_pack's pstate)
 constexpr int TRIP_WORDS = 64;
 constexpr int DPEND_WORDS = 64;
+constexpr int PART_WORDS = 64;
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
-         TRIP_WORDS + DPEND_WORDS;
+         TRIP_WORDS + DPEND_WORDS + PART_WORDS;
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
@@ -418,6 +453,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   tripsL[lane] = 0;          // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
   uint32_t* const dpend = tripsL + TRIP_WORDS;      // (likewise)
   dpend[lane] = 0;
+  uint32_t* const pcache = dpend + DPEND_WORDS;    // [CPW] epochs, then [CPW] draws
   __builtin_amdgcn_wave_barrier();
 
   // RAFT_SCHED_ALIGNED launches a grid sized for the padded packing; waves past its slots exit.
@@ -425,6 +461,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   if (wave * CPW >= nslots) return;
   do {
     if (CATCH) tripsL[lane] = 0;
+    if (lane < CPW) pcache[lane] = INF;               // no partition epoch drawn yet
     const int cs = lane / N, k0 = lane - cs * N;
     const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
     const uint32_t c0 = lane < CPW * N && slot < nslots ? (perm ? perm[slot] : slot) : INF;
@@ -957,19 +994,27 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 uint32_t* cl =
                     mycells + (k * (N - 1) + (dst - 1 < (uint32_t)k ? dst - 1 : dst - 2)) * CELLW;
                 cell_put(cl, make_uint4(RAFT_MSG_CLIENT_SET, 0, 0, mb + 1), make_uint4(0, 0, 0, 0));
-                cl[CELLW - 1] = 1u | 1u << 16;
+                cl[CELLW - 1] = 1u | 1u << 16;     // one copy at t + 1 (SIM_SPEC D15)
               }
               sentmask |= 1u << dst;
             }
           }
           // ------------------------------------------------ emission (rpc / respond)
+          // The message words go to the pair cells, then each message's fault draws (its delivery
+          // pack, in the cell's last word) and the receiver's bit into sentmask.
           if (emit) {
-            bool part = false;
-            uint32_t sides = 0;
+            // the cluster's partition draw for this tick's epoch, made once per epoch (SIM_SPEC P2)
+            uint32_t pstate = 0;
             if (!LITE && S.part_ppm) {
-              const uint4 pw = philox(sg, P_PART << 8, udiv(S.div_epoch, t), 0, S.key0, S.key1);
-              part = ppm(pw.x) < S.part_ppm;
-              sides = pw.y;
+              const int cw = bl / N;
+              const uint32_t e = udiv(S.div_epoch, t);
+              pstate = pcache[CPW + cw];
+              if (pcache[cw] != e) {
+                const uint4 pw = philox(sg, P_PART << 8, e, 0, S.key0, S.key1);
+                pstate = (pw.y & ~1u) | (ppm(pw.x) < S.part_ppm ? 1u : 0u);
+                pcache[cw] = e;          // (the cluster's lanes that draw write the same words)
+                pcache[CPW + cw] = pstate;
+              }
             }
             *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
                 emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
@@ -978,63 +1023,66 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
               cell_put(cl, ra, rb);
               lctr_add(lctr, RAFT_CTR_SENT, 1);
-              transmit<N, LITE>(S, sg, t, id, src, part, sides, cl, sentmask, lctr);
+              const uint32_t pack = deliver_pack<LITE>(S, sg, t, id, src, pstate, lctr);
+              cl[CELLW - 1] = pack;
+              if (pack >> 16) sentmask |= 1u << src;
             } else {
-              // Message words first, for every peer at once: the next-index loads (and then the
-              // prev-entry loads) of all peers are independent, so they overlap instead of paying
-              // one memory round trip per peer; the fault draws follow in a compact loop.
-              int32_t nxs[N];
+              // Message words for every peer at once: the next-index reads and then the prev-entry
+              // loads of all peers are independent and issued together (one memory round trip for
+              // the broadcast); a slot is always read, inside the arena, and used only when needed.
+              if (emit == 2) {
+                // prev of peer p (SPEC: SIM_SPEC §8's clamp(next - 1); faithful: core.clj:59-66's
+                // max(next - 1, 0), whose entry is at min(prev, len)), read twice from the rows
+                auto prev_of = [&](int p) -> uint32_t {
+                  const int32_t pv = lsw.next(p) - 1;
+                  if constexpr (SPEC) return pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
+                  return pv > 0 ? (uint32_t)pv : 0u;
+                };
+                const uint32_t bm = n.base % A;
+                uint2 e[N];
   #pragma unroll
-              for (int p = 0; p < N; ++p) nxs[p] = emit == 2 ? lsw.next(p) : 0;
-  #pragma unroll 1
-              for (int p = 1; p <= N; ++p) {
-                if (p == (int)id) continue;
-                if (SPEC && emit == 2) {                    // SIM_SPEC §8 broadcast
-                  const int32_t pv = nxs[p - 1] - 1;
-                  const uint32_t prev = pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
-                  uint32_t ep = 0, et = 0, evl = 0;
-                  if (prev) {
-                    const uint2 e = sar[(n.base + prev - 1) % A];
-                    ep = 1; et = e.x; evl = e.y;
-                  }
-                  const uint32_t pc = n.len - prev;
-                  pmax = pc > pmax ? pc : pmax;
-                  ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
-                                  n.commit, prev);
-                  rb = make_uint4(et, evl, pc ? n.base + prev : 0, 0);
-                } else if (emit == 2) {
-                  const int32_t nx = nxs[p - 1];
-                  const int32_t prev = nx - 1 > 0 ? nx - 1 : 0;
-                  const uint32_t start = (uint32_t)prev < n.len ? (uint32_t)prev : n.len;
-                  uint32_t ep = 0, et = 0, evl = 0, pc = 0, po = 0;
-                  if (start < n.len) {
-                    const uint2 e = sar[(n.base + start) % A];
-                    ep = 1; et = e.x; evl = e.y;
-                    pc = n.len - start - 1;
-                    po = pc ? n.base + start + 1 : 0;
-                  }
-                  pmax = pc > pmax ? pc : pmax;
-                  ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
-                                  n.commit, (uint32_t)prev);
-                  rb = make_uint4(et, evl, po, 0);
+                for (int p = 0; p < N; ++p) {
+                  const uint32_t prev = prev_of(p);
+                  const uint32_t at = SPEC ? (prev ? prev - 1 : 0u) : (prev < n.len ? prev : 0u);
+                  uint32_t slot = bm + at;
+                  slot = slot >= A ? slot - A : slot;
+                  e[p] = sar[slot];
                 }
-                cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
+  #pragma unroll
+                for (int p = 1; p <= N; ++p) {
+                  if (p == (int)id) continue;
+                  const uint2 ep2 = e[p - 1];
+                  const uint32_t prev = prev_of(p - 1);
+                  if constexpr (SPEC) {
+                    const uint32_t ep = prev ? 1u : 0u;
+                    const uint32_t pc = n.len - prev;
+                    pmax = pc > pmax ? pc : pmax;
+                    ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | ep << 8 | pc << 16, n.term,
+                                    n.commit, prev);
+                    rb = make_uint4(ep ? ep2.x : 0u, ep ? ep2.y : 0u, pc ? n.base + prev : 0, 0);
+                  } else {
+                    const uint32_t start = prev < n.len ? prev : n.len;
+                    const bool has = start < n.len;
+                    const uint32_t pc = has ? n.len - start - 1 : 0u;
+                    pmax = pc > pmax ? pc : pmax;
+                    ra = make_uint4(RAFT_MSG_APPEND_ENTRIES | id << 3 | (has ? 1u : 0u) << 8 | pc << 16,
+                                    n.term, n.commit, prev);
+                    rb = make_uint4(has ? ep2.x : 0u, has ? ep2.y : 0u, pc ? n.base + start + 1 : 0u, 0);
+                  }
+                  cell_put(mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW, ra, rb);
+                }
+              } else {                                // request-vote: the same words for every peer
+  #pragma unroll
+                for (int j = 0; j < N - 1; ++j) cell_put(mycells + (k * (N - 1) + j) * CELLW, ra, rb);
               }
               if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
               lctr_add(lctr, RAFT_CTR_SENT, N - 1);
-              if constexpr (LITE) {          // every peer gets one copy after the fixed delay
-  #pragma unroll
-                for (int j = 0; j < N - 1; ++j)
-                  mycells[(k * (N - 1) + j) * CELLW + CELLW - 1] = S.dmin | 1u << 16;
-                sentmask |= peers;
-              } else {
   #pragma unroll 1
-                for (int p = 1; p <= N; ++p) {
-                  if (p == (int)id) continue;
-                  transmit<N, LITE>(S, sg, t, id, p, part, sides,
-                              mycells + (k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW,
-                              sentmask, lctr);
-                }
+              for (int p = 1; p <= N; ++p) {
+                if (p == (int)id) continue;
+                const uint32_t pack = deliver_pack<LITE>(S, sg, t, id, (uint32_t)p, pstate, lctr);
+                mycells[(k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW + CELLW - 1] = pack;
+                if (pack >> 16) sentmask |= 1u << p;
               }
             }
           }
@@ -1090,7 +1138,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           const uint32_t pold_len = n.len - m;
           // physical slots advance with a wrap instead of a per-entry modulo
           if (preloc)
-            arena_copy<LITE ? 1 : 4>(sar, n.base % A, sar, pold_base % A, pold_len, A);
+            arena_copy<LITE ? 1 : 8>(sar, n.base % A, sar, pold_base % A, pold_len, A);
           uint32_t di = (n.base + pold_len) % A;
           if (pkind == PLAN_ENTRY) {
             sar[di] = make_uint2(ppoff, ppcnt);
@@ -1104,18 +1152,22 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               sar[di] = make_uint2(0, 0);
               di = di + 1 == A ? 0 : di + 1;
             }
-            arena_copy<LITE ? 1 : 4>(sar, di, sa, si, m - evicted, A);
+            arena_copy<LITE ? 1 : 8>(sar, di, sa, si, m - evicted, A);
             lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
           }
         }
         if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
           uint32_t cc = S.ccount[sgi];
-          uint32_t si = (n.base + n.commit - papplied) % A;
-          for (uint32_t i = 0; i < papplied; ++i, ++cc) {
-            if (S.SC) S.stream[(size_t)sgi * S.SC + cc % S.SC] = sar[si].y;
-            si = si + 1 == A ? 0 : si + 1;
+          if (S.SC) {
+            uint32_t si = (n.base + n.commit - papplied) % A, so = cc % S.SC;
+            uint32_t* const ring = S.stream + (size_t)sgi * S.SC;
+            for (uint32_t i = 0; i < papplied; ++i) {
+              ring[so] = sar[si].y;
+              si = si + 1 == A ? 0 : si + 1;
+              so = so + 1 == S.SC ? 0 : so + 1;
+            }
           }
-          S.ccount[sgi] = cc;
+          S.ccount[sgi] = cc + papplied;
         }
         if constexpr (TRACE) {   // the traced message's :entries, resolved like the payload above
           const uint32_t tfront = __shfl(n.front, bl + (int)tr_src - 1);
@@ -1147,29 +1199,65 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         }
         if (__ballot(appended_at >= 0)) {              // log matching
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
-          // Transposed: for each node a that appended, every peer lane compares its own log with
-          // a's new entries at once (the peers' loads are in flight together, one memory round
-          // trip per W positions instead of one per peer), and a counts one violation if any
-          // peer found a position with the same term and another value.
-          bool bad = false;
-          // node indices a that appended in some cluster of the wave (lane l is node l mod N of
-          // its cluster): the others are skipped with scalar tests only
-          const uint64_t apm = __ballot(active && appended_at >= 0);
-  #pragma unroll 1
-          for (int a = 0; a < N; ++a) {
-            if (!(apm & node_lanes<N>(a))) continue;
-            const int32_t aat = __shfl(appended_at, bl + a);
-            const uint32_t ab = __shfl(n.base, bl + a), al = __shfl(n.len, bl + a);
-            bool c = false;
-            if (active && aat >= 0 && a != k) {
-              const uint32_t hi = al < n.len ? al : n.len, lo = (uint32_t)aat;
-              if (hi > lo)
-                c = log_conflict<LITE ? 1 : 4>(arena_of(S, sgi - k + a), (ab + lo) % A, sar,
-                                               (n.base + lo) % A, hi - lo, A);
+          // Each lane b compares its own log with the new entries of every other node a of its
+          // cluster that appended this tick, pair after pair, W positions per trip of one
+          // wave-wide loop (a wave runs as many trips as its busiest lane needs, not the sum over
+          // node indices of the busiest lane per index); a counts one violation if any peer found
+          // a position with the same term and another value. The appenders' (appended_at, base,
+          // len) go through LDS (the cells: P2 is done with them) so a lane can read any
+          // appender's words from inside the divergent loop.
+          uint32_t* const apw = cells;
+          apw[lane] = (uint32_t)appended_at;
+          apw[64 + lane] = n.base;
+          apw[128 + lane] = n.len;
+          __builtin_amdgcn_wave_barrier();
+          const uint32_t apc = (uint32_t)(__ballot(active && appended_at >= 0) >> bl) & cmask;
+          uint32_t todo = active ? apc & ~(1u << k) : 0u;
+          uint32_t found = 0, cur = 0, rem = 0, xi = 0, yi = 0;
+          const uint2* xa = sar;
+          constexpr int W = LITE ? 1 : 8;
+          while (__ballot(todo || rem)) {
+            if (!rem && todo) {
+              const int a = __builtin_ctz(todo);
+              todo &= todo - 1;
+              const uint32_t aat = apw[bl + a], ab = apw[64 + bl + a], al = apw[128 + bl + a];
+              const uint32_t hi = al < n.len ? al : n.len;
+              rem = hi > aat ? hi - aat : 0u;
+              xi = (ab + aat) % A;
+              yi = (n.base + aat) % A;
+              xa = arena_of(S, sgi - k + a);
+              cur = (uint32_t)a;
             }
-            const bool any = cluster_any(c);           // (a wave-wide ballot: every lane)
-            bad |= active && a == k && any;            // (idle lanes past the clusters alias one)
+            if (rem) {
+              const uint32_t c = min(min(rem, (uint32_t)W), min(A - xi, A - yi));
+              const uint2* xp = xa + xi;
+              const uint2* yp = sar + yi;
+              uint2 x[W], y[W];
+  #pragma unroll
+              for (int j = 0; j < W; ++j) {
+                x[j] = xp[j];
+                y[j] = yp[j];
+              }
+              bool hit = false;
+  #pragma unroll
+              for (int j = 0; j < W; ++j)
+                hit |= (uint32_t)j < c && x[j].x == y[j].x && x[j].y != y[j].y;
+              if (hit) {
+                found |= 1u << cur;
+                rem = 0;
+              } else {
+                rem -= c;
+                xi += c;
+                yi += c;
+                xi = xi == A ? 0 : xi;
+                yi = yi == A ? 0 : yi;
+              }
+            }
           }
+          uint32_t fa = 0;
+  #pragma unroll
+          for (int s = 0; s < N; ++s) fa |= (uint32_t)__shfl((int)found, bl + s);
+          const bool bad = active && ((fa >> k) & 1);
           if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
         }
         if (elected && hidx > 0) {                     // leader completeness (pre-tick hwm)

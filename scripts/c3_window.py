@@ -1,5 +1,6 @@
 """C3 from init-node, per-launch tick-kernel time over a window, per build (diagnostic).
-Usage: c3_window.py CLUSTERS STEPS LIB [LIB ...]"""
+Usage: [SPEC=1] c3_window.py CLUSTERS STEPS LIB [LIB ...]   (SPEC=1: the C3-spec workload)"""
+import os
 import sys
 from pathlib import Path
 
@@ -10,6 +11,8 @@ from raftsim._backend import Backend  # noqa: E402
 C, K = int(sys.argv[1]), int(sys.argv[2])
 CFG = dict(nodes=5, seed=1, log_cap=256, client_ppm=80000, client_period=16384, client_burst=2048,
            client_redirects=4, drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
+if os.environ.get("SPEC") == "1":
+    CFG.update(variant_flags=2, log_cap=1024)
 res = {}
 for lib in sys.argv[3:]:
     sim = Backend(lib, "raft_sim_", n_clusters=C, **CFG)
