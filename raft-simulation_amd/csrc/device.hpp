@@ -29,7 +29,7 @@ enum { PLAN_NONE = 0, PLAN_PAYLOAD = 1, PLAN_ENTRY = 2 };
 constexpr int LCTR_FIRSTVIOL = RAFT_CTR_COUNT;       // per-wave LDS slot: min violation tick
 constexpr int LCTR_PAYLOADMAX = RAFT_CTR_COUNT + 1;  // per-wave LDS slot: max AE payload
 constexpr int LCTR_WORDS = 32;
-constexpr int PW_WORDS = 64;    // 32 x u64 client-gap powers at the start of the wave's LDS
+constexpr int PW_WORDS = 32;    // the 32 client-gap powers' low words at the start of the wave's LDS
 static_assert(LCTR_PAYLOADMAX < LCTR_WORDS, "counter block");
 // Waves flush their counters into one of CTR_COPIES copies of the counter block (wave index mod
 // CTR_COPIES): thousands of waves ending together otherwise serialise on the same few words of
@@ -177,25 +177,40 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
 // Geometric gap G(w) of SIM_SPEC §4 P0: the greedy power search over pw[top..0] (higher powers
 // are 0 and never fire). The accumulator starts at 2^32 and every power is below 2^32 when
 // client_ppm > 0, so after its first step it fits 32 bits and (acc * pw) >> 32 is one
-// v_mul_hi_u32 instead of a 64x64-bit product.
-// pw: the wave's LDS copy of the table (scalar loads from the kernel argument's copy measured
-// slower: each step waits on its own load).
-__device__ inline uint64_t client_gap(uint32_t w, const unsigned long long* pw, int top) {
+// v_mul_hi_u32 instead of a 64x64-bit product; c >= w + 1 is c > w. pw: the low words of the
+// powers (the wave's LDS copy, or the kernel argument's u64 table). The low GAP_UNROLL powers
+// are loaded together before the chain (the accumulator does not decide which power a step
+// reads), so a step costs its multiply and select rather than a load's latency: 600 -> ~ cycles
+// per draw at four waves per SIMD (scripts/p0_probe.hip; a loop with a load per step waited on
+// each); powers above them (client_ppm < ~2 %) take a step per loop trip first.
+constexpr int GAP_UNROLL = 12;
+template <typename T>
+__device__ inline uint64_t client_gap(uint32_t w, const T* pw, int top) {
   // client_ppm == 0 (top == 32; reachable only through a host-written client cursor): every
   // power is 2^32, so the search takes every step
   if (top > 31) return 0xFFFFFFFFull;
-  const uint64_t u = (uint64_t)w + 1;
-  uint32_t acc = 0;
+  uint32_t acc = 0, g = 0;
   bool full = true;                 // acc == 2^32
-  uint64_t g = 0;
-  for (int i = top; i >= 0; --i) {
+  int i = top;
+  for (; i >= GAP_UNROLL; --i) {
     const uint32_t p = (uint32_t)pw[i];
     const uint32_t c = full ? p : __umulhi(acc, p);
-    if ((uint64_t)c >= u) {
+    if (c > w) {
       acc = c;
       full = false;
-      g += 1ull << i;
+      g += 1u << i;
     }
+  }
+  uint32_t p[GAP_UNROLL];
+#pragma unroll
+  for (int j = 0; j < GAP_UNROLL; ++j) p[j] = (uint32_t)pw[j];
+#pragma unroll
+  for (int j = GAP_UNROLL - 1; j >= 0; --j) {
+    const uint32_t c = full ? p[j] : __umulhi(acc, p[j]);
+    const bool fire = j <= i && c > w;
+    acc = fire ? c : acc;
+    full = full && !fire;
+    g += fire ? 1u << j : 0u;
   }
   return g;
 }
@@ -212,7 +227,7 @@ __device__ inline uint32_t on_tick(uint64_t j, uint32_t P, const DivU32& B) {
 }
 // The next injection after the one at tick t (an on-tick), drawing gap word w.
 __device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const DevSim& S,
-                                            const unsigned long long* pw) {
+                                            const uint32_t* pw) {
   const uint32_t P = S.client_period;
   const uint32_t q = P ? udiv(S.div_period, t) : 0u;
   const uint64_t j = P ? (uint64_t)q * S.div_burst.d + (t - q * P) : t;
@@ -263,7 +278,9 @@ struct QueueR {
 // Node registers held by one lane for a whole launch. Queues are named fields (never indexed by a
 // runtime value) so that they stay in VGPRs.
 struct NodeR {
-  uint32_t role, vf, lid, fault, seq, lsp, votes, keys;
+  // keys: the leader-state's peer keys (bits 1..N) and, in bit 0, whether it is present (ls_present;
+  // a state with keys but no leader-state is rejected by raft_sim_write_nodes)
+  uint32_t role, vf, lid, fault, seq, votes, keys;
   uint32_t term, commit, len, deadline;
   QueueR rq, rs;
   uint32_t base, front, led;

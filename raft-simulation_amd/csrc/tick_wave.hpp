@@ -87,8 +87,8 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
   w[0] = t; w[1] = seq;
   w[2] = m0.x; w[3] = m0.y; w[4] = m0.z; w[5] = m0.w;
   w[6] = m1.x; w[7] = m1.y; w[8] = m1.z; w[9] = m1.w;
-  w[10] = n.role | n.vf << 8 | n.lid << 16 | n.lsp << 24;
-  w[11] = n.votes | n.keys << 16;
+  w[10] = n.role | n.vf << 8 | n.lid << 16 | (n.keys & 1u) << 24;
+  w[11] = n.votes | (n.keys & ~1u) << 16;
   w[12] = n.term;
 #pragma unroll
   for (int p = 0; p < RAFT_MAX_NODES; ++p) {
@@ -217,7 +217,7 @@ __device__ __forceinline__ void spec_handle(
   if (fault) return;
   if (type != RAFT_MSG_CLIENT_SET && mterm > n.term) {          // term rule: step down
     n.term = mterm; n.vf = 0; n.votes = 0; n.lid = 0; n.role = RAFT_FOLLOWER;
-    if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
+    if (n.keys & 1u) { n.keys = 0; nm = 2; }
   }
   switch (type) {
     case RAFT_MSG_REQUEST_VOTE: {
@@ -240,7 +240,7 @@ __device__ __forceinline__ void spec_handle(
       if (mterm < n.term) break;
       n.role = RAFT_FOLLOWER; n.votes = 0; n.lid = src;
       rearm = true;                         // AppendEntries from the current leader
-      if (n.lsp) { n.lsp = 0; n.keys = 0; nm = 2; }
+      if (n.keys & 1u) { n.keys = 0; nm = 2; }
       if (!consistent) break;
       // first conflict in [b, min(len, b + pcnt)); the payload is read from the sender's arena,
       // an entry its pre-tick frontier has overwritten reading (0, 0)
@@ -334,7 +334,7 @@ __device__ __forceinline__ void spec_handle(
         break;
       }
       n.role = RAFT_LEADER; n.votes = 0; n.lid = id;              // voted_for kept
-      n.lsp = 1; n.keys = peers;
+      n.keys = peers | 1u;
       nm = 1;
       emit = 2;
       elected = true;
@@ -442,8 +442,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
   // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters, leader rows and
   // per-lane words
-  unsigned long long* pw = reinterpret_cast<unsigned long long*>(smem);
-  if (lane < 32) pw[lane] = S.client_pw[lane];
+  uint32_t* const pw = smem;
+  if (lane < 32) pw[lane] = (uint32_t)S.client_pw[lane];
   uint32_t* cells = smem + PW_WORDS;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
@@ -482,8 +482,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     if (active) {
       const uint32_t fl = hp[HF_FLAGS * N], mk = hp[HF_MASKS * N], qm = hp[HF_QMETA * N];
       n.role = fl & 3; n.vf = (fl >> 2) & 15; n.lid = (fl >> 6) & 15; n.fault = (fl >> 10) & 7;
-      n.seq = (fl >> 13) & 1; n.lsp = (fl >> 14) & 1;
-      n.votes = mk & 0xFFFF; n.keys = mk >> 16;
+      n.seq = (fl >> 13) & 1;
+      n.votes = mk & 0xFFFF; n.keys = mk >> 16 | ((fl >> 14) & 1);
       n.term = hp[HF_TERM * N]; n.commit = hp[HF_COMMIT * N]; n.len = hp[HF_LEN * N];
       n.deadline = hp[HF_DEADLINE * N];
       n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
@@ -555,10 +555,18 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       wl_kmin = wave_min(key);
       wl_kmax = ~wave_min(key == INF ? ~0u : ~key);
     }
-    // per-phase shader cycles summed over the wave's trips, stamped at wave-uniform points only:
-    // 0 P0, 3 P1, 4 P2, 5 P3, 6 P4, 7 the append-response drain, 8 the trip's loop head (next
-    // event, exit ballot); 9 the launch-start state load
-    uint32_t wl_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // per-phase shader cycles summed over the wave's trips, stamped where the wave enters a block
+    // (a skipped stamp merges its interval into the next): 11 P0's draws, 0 P0's queue insert, 1
+    // P1's queue pop, 2 the handler, 10 timer/hash/counters, 3 redirects, emission and fault
+    // draws, 4 P2, 5 P3, 6 P4, 7 the append-response drain, 8 the trip's loop head (next event,
+    // exit ballot); 9 the launch-start state load
+    uint32_t wl_ph[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // wave-level passes of each Philox call site (the first active lane counts the pass; summed
+    // over the lanes at the end): 0 client, 1 deferred timer, 2 alts!!, 3 Spec re-arm, 4 redirect, 5 partition,
+    // 6 fault draws of replies, 7 fault draws of broadcasts (per peer)
+    uint32_t wl_px0 = 0, wl_px1 = 0, wl_px2 = 0, wl_px3 = 0, wl_px4 = 0, wl_px5 = 0, wl_px6 = 0,
+             wl_px7 = 0;
+  #define RS_PX(v) (v) += (uint32_t)(lane == (int)__builtin_ctzll(__ballot(1)))
     uint64_t wl_ts = 0;
     const uint64_t wl_mt0 = __builtin_amdgcn_s_memtime();
   #define RS_PHASE(i)                                          \
@@ -569,6 +577,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     } while (0)
   #else
   #define RS_PHASE(i) do {} while (0)
+  #define RS_PX(v) do {} while (0)
   #endif
 
 
@@ -628,6 +637,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #endif
       if (!LITE && __ballot(cinj)) {
         if (cinj) {
+          RS_PX(wl_px0);
           const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
           if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
           if (1 + __umulhi(d.y, N) == id) {
@@ -638,6 +648,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           cnext = client_next_tick(t, d.w, S, pw);
         }
       }
+      RS_PHASE(11);
 
       // A client-set that lands in an empty REQ queue would be its head at arrival t, so it is
       // kept in registers (dcs) instead of a global store + same-tick load; it is written to the
@@ -668,6 +679,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // A deferred timer draw due at this tick with no message ready: its own tick's draw
       // (deadline - el_base) decides whether the node times out now.
       if (!SPEC && live && dpend[lane] && !req_ok && !res_ok && n.deadline <= t) {
+        RS_PX(wl_px1);
         const uint4 wd = event_draw(sg, id, n.deadline - S.el_base, S);
         n.deadline += __umulhi(wd.y, S.el_span);
         dpend[lane] = 0;
@@ -680,6 +692,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         bool have_w = false;
         int which = -1;
         if (req_ok && res_ok) {
+          RS_PX(wl_px2);
           w = event_draw(sg, id, t, S);
           have_w = true;
           which = (w.x & 1) ? 1 : 0;
@@ -731,6 +744,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                        mpoff = m1.w;
   #ifdef RS_WAVELOG
         asm volatile("" ::"v"(hdr), "v"(mb));   // the pop's wait lands before the stamp
+        RS_PHASE(1);
   #endif
         const uint32_t type = hdr & 7, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1,
                        mep = (hdr >> 8) & 1, pcnt = hdr >> 16;
@@ -765,7 +779,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             // (- nil 1) and subvec of a LazySeq
             const uint32_t first = id == 1 ? 2u : 1u;
             if (n.commit > n.len) fault = RAFT_FAULT_IOOBE;
-            else if (!n.lsp || !((n.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
+            else if (!(n.keys & 1u) || !((n.keys >> first) & 1)) fault = RAFT_FAULT_NPE;
             else if (n.seq) fault = RAFT_FAULT_CCE;
             else if ((n.keys & peers) != peers) fault = RAFT_FAULT_NPE;
             else emit = 2;
@@ -888,7 +902,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   fault = RAFT_FAULT_CCE;      // append-entries-rpc's entries-from (log.clj:53)
                 } else {                                       // candidate->leader 80-84
                   n.role = RAFT_LEADER; n.vf = 0; n.votes = 0; n.lid = id;
-                  n.lsp = 1; n.keys = peers;                   // leader-state 40-42
+                  n.keys = peers | 1u;                         // leader-state 40-42
                   nm = 1;
                   emit = 2;
                   elected = true;
@@ -899,17 +913,16 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             case RAFT_MSG_APPEND_RESPONSE: {                   // append-response-handler 141-149
               if (mterm > n.term) {                            // leader->follower 86-89
                 n.term = mterm;
-                n.role = RAFT_FOLLOWER; n.lid = 0; n.lsp = 0; n.keys = 0;
+                n.role = RAFT_FOLLOWER; n.lid = 0; n.keys = 0;
                 nm = 2;
               } else if (!flag) {
-                if (!n.lsp || !((n.keys >> src) & 1)) {
+                if (!(n.keys & 1u) || !((n.keys >> src) & 1)) {
                   fault = RAFT_FAULT_NPE;                      // (dec nil)
                   break;
                 }
                 nm = 3;
               } else {
-                n.lsp = 1;
-                n.keys |= 1u << src;
+                n.keys |= 1u | 1u << src;
                 nm = 4;
                 mchg = true;
               }
@@ -919,6 +932,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               break;
           }
         }
+        RS_PHASE(2);
         const uint32_t tsrc = which >= 0 ? src : 0, tterm = which >= 0 ? mterm : 0;
         if (fault) {                                   // D8: halted with the pre-event state
           n.fault = fault;
@@ -971,6 +985,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             lctr_add(lctr, RAFT_CTR_LEADERS, 1);
             n.led = n.term;
           }
+          RS_PHASE(10);
           // ------------------------------------------------ redirect-client (server.clj:62-63)
           // to the :leader-id, else (rand-nth cluster) by w2 of the EVENT draw (core.clj:153-155);
           // the client follows it while the message has hops left (SIM_SPEC D15): a client-set
@@ -983,7 +998,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             } else {
               uint32_t dst = n.lid;
               if (!dst) {
-                if (!have_w) w = event_draw(sg, id, t, S);   // (the timer stays deferred)
+                if (!have_w) { RS_PX(wl_px4); w = event_draw(sg, id, t, S); }   // (the timer stays deferred)
                 const uint32_t i = __umulhi(w.z, N - 1);
                 dst = i + 1 < id ? i + 1 : i + 2;
               }
@@ -999,6 +1014,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               sentmask |= 1u << dst;
             }
           }
+          RS_PHASE(12);
           // ------------------------------------------------ emission (rpc / respond)
           // The message words go to the pair cells, then each message's fault draws (its delivery
           // pack, in the cell's last word) and the receiver's bit into sentmask.
@@ -1010,6 +1026,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               const uint32_t e = udiv(S.div_epoch, t);
               pstate = pcache[CPW + cw];
               if (pcache[cw] != e) {
+                RS_PX(wl_px5);
                 const uint4 pw = philox(sg, P_PART << 8, e, 0, S.key0, S.key1);
                 pstate = (pw.y & ~1u) | (ppm(pw.x) < S.part_ppm ? 1u : 0u);
                 pcache[cw] = e;          // (the cluster's lanes that draw write the same words)
@@ -1023,6 +1040,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   mycells + (k * (N - 1) + (src - 1 < (uint32_t)k ? src - 1 : src - 2)) * CELLW;
               cell_put(cl, ra, rb);
               lctr_add(lctr, RAFT_CTR_SENT, 1);
+              RS_PX(wl_px6);
               const uint32_t pack = deliver_pack<LITE>(S, sg, t, id, src, pstate, lctr);
               cl[CELLW - 1] = pack;
               if (pack >> 16) sentmask |= 1u << src;
@@ -1080,6 +1098,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #pragma unroll 1
               for (int p = 1; p <= N; ++p) {
                 if (p == (int)id) continue;
+                RS_PX(wl_px7);
                 const uint32_t pack = deliver_pack<LITE>(S, sg, t, id, (uint32_t)p, pstate, lctr);
                 mycells[(k * (N - 1) + (p - 1 < k ? p - 1 : p - 2)) * CELLW + CELLW - 1] = pack;
                 if (pack >> 16) sentmask |= 1u << p;
@@ -1365,7 +1384,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15,
                                  flag = (hdr >> 7) & 1;
                   if (!((hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
-                        (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1))))
+                        (flag ? n.len <= hidx : (n.keys & 1u) && ((n.keys >> src) & 1))))
                     break;
                   QueueR r = n.rs;
                   r.h = nh;
@@ -1375,8 +1394,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   if (!r.c) r.h = 0;
                   n.rs = r;
                   if (flag) {                                // append-response-handler 145-149
-                    n.lsp = 1;
-                    n.keys |= 1u << src;
+                    n.keys |= 1u | 1u << src;
                     lsw.next(src - 1) = (int32_t)m1.x;
                     lsw.match(src - 1) = (int32_t)m0.w;
                   } else {                                   // 143-144: (dec next-index)
@@ -1411,7 +1429,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               }
               const uint32_t hdr = m0.y, mterm = m0.z, src = (hdr >> 3) & 15, flag = (hdr >> 7) & 1;
               const bool simple = (hdr & 7) == RAFT_MSG_APPEND_RESPONSE && mterm <= n.term &&
-                                  (flag ? n.len <= hidx : n.lsp && ((n.keys >> src) & 1));
+                                  (flag ? n.len <= hidx : (n.keys & 1u) && ((n.keys >> src) & 1));
               // a tick at which any node of the cluster needs the loop above is the loop's to run
               dr = dr && !cluster_any(hbeat || (ev && !simple));
               if (!__ballot(dr)) break;
@@ -1424,8 +1442,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 if (!r.c) r.h = 0;
                 n.rs = r;
                 if (flag) {                                  // append-response-handler 145-149
-                  n.lsp = 1;
-                  n.keys |= 1u << src;
+                  n.keys |= 1u | 1u << src;
                   lsw.next(src - 1) = (int32_t)m1.x;
                   lsw.match(src - 1) = (int32_t)m0.w;
                 } else {                                     // 143-144: (dec next-index)
@@ -1448,6 +1465,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       tnext = t + 1;
     }
   #ifdef RS_WAVELOG
+    uint32_t wl_px[8] = {wl_px0, wl_px1, wl_px2, wl_px3, wl_px4, wl_px5, wl_px6, wl_px7};
+  #pragma unroll
+    for (int q = 0; q < 8; ++q)
+  #pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wl_px[q] += (uint32_t)__shfl_xor((int)wl_px[q], o);
     if (lane == 0 && S.wavelog) {
       const uint64_t wl_end = wall_clock64();
       uint32_t hw, xcc;
@@ -1460,7 +1482,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       rec[2] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
       rec[3] = make_uint4(wl_ph[4], wl_ph[5], wl_ph[6], wl_ph[7]);
       rec[4] = make_uint4(wl_ph[8], wl_ph[9], wl_ph[10], wl_ph[11]);
-      rec[5] = make_uint4(wl_drain, wl_inj, wl_dead, 0);
+      rec[5] = make_uint4(wl_drain, wl_inj, wl_dead, wl_ph[12]);
+      rec[6] = make_uint4(wl_px[0], wl_px[1], wl_px[2], wl_px[3]);
+      rec[7] = make_uint4(wl_px[4], wl_px[5], wl_px[6], wl_px[7]);
     }
   #endif
 
@@ -1501,8 +1525,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       }
     }
     if (active) {
-      hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.lsp);
-      hp[HF_MASKS * N] = n.votes | n.keys << 16;
+      // the block's addresses again from the cluster index (held across the tick loop they would
+      // take four VGPRs there)
+      uint32_t cw = c;
+      asm volatile("" : "+v"(cw));
+      uint32_t* const hp = S.hot + (size_t)cw * HB + HOT_CW + k0;
+      uint32_t* const hc = S.hot + (size_t)cw * HB + CLW;
+      hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.keys & 1u);
+      hp[HF_MASKS * N] = n.votes | (n.keys & ~1u) << 16;
       hp[HF_TERM * N] = n.term; hp[HF_COMMIT * N] = n.commit; hp[HF_LEN * N] = n.len;
       hp[HF_DEADLINE * N] = n.deadline;
       hp[HF_QMETA * N] = pack_qmeta(n.rq.h, n.rq.c, n.rs.h, n.rs.c);

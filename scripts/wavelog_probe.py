@@ -68,14 +68,21 @@ print("per-SIMD summed wave-us p0/50/100:", b.min(), np.median(b), b.max())
 per_xcc = [np.median(life[xcc == x]) for x in range(8)]
 print("per-XCC median life:", " ".join(f"{v:.1f}" for v in per_xcc))
 # wave-uniform phase stamps (shader cycles per wave, summed over its trips): rec[2..4] = ph0..11
-ph = a[:, [8, 11, 12, 13, 14, 15, 16]].astype(np.float64)
-names = ("P0", "P1", "P2", "P3", "P4", "drain", "loop-head")
+# rec[2..4] = ph0..11: 11 P0 draws, 0 P0 insert, 1 pop, 2 handler, 10 timer/hash, 3 emission,
+# 4 P2, 5 P3, 6 P4, 7 drain, 8 loop head
+ph = a[:, [19, 8, 9, 10, 18, 23, 11, 12, 13, 14, 15, 16]].astype(np.float64)
+names = ("P0-draw", "P0-ins", "P1-pop", "P1-hdl", "P1-tmr", "P1-redir", "P1-emit", "P2", "P3", "P4",
+         "drain", "loop-head")
 tot = ph.sum(axis=1)
 trips = np.maximum(act, 1)[:, None]
 print("phase cycles per trip (mean over waves): " + "  ".join(
     f"{nm} {v:7.0f}" for nm, v in zip(names, (ph / trips).mean(axis=0))))
 print("phase cycles per wave (mean): " + "  ".join(
     f"{nm} {v:8.0f}" for nm, v in zip(names, ph.mean(axis=0))) + f"  load {a[:, 17].mean():8.0f}")
+px = a[:, 24:32].astype(np.float64)
+print("Philox passes per wave (mean): " + "  ".join(
+    f"{nm} {v:7.1f}" for nm, v in zip(("client", "deferred", "alts", "spec-rearm", "redirect",
+                                         "partition", "reply-net", "bcast-net"), px.mean(axis=0))))
 print("drained ticks per wave p0/10/50/90/99/100:", q(a[:, 20]))
 print("client-injection ticks per wave p0/10/50/90/99/100:", q(a[:, 21]))
 print("dead clusters per wave at launch start p0/10/50/90/99/100:", q(a[:, 22]))
