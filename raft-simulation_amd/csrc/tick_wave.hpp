@@ -635,8 +635,16 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #ifdef RS_WAVELOG
       wl_inj += __ballot(cinj) ? 1 : 0;
   #endif
-      if (!LITE && __ballot(cinj)) {
-        if (cinj) {
+      // The EVENT draw of this tick (alts!! bit, timer, rand-nth redirect) rides in the same Philox
+      // pass as the client draw: the cluster's first lane draws for the client and shares the words,
+      // and every other lane that may take a client-set without a leader id to redirect to (the
+      // redirect storm of a leaderless burst) draws its EVENT word now instead of in P1 -- one pass
+      // for both where there were two. The draw is the same one P1 would make (keyed by node and
+      // tick), so nothing but the pass count changes.
+      uint4 w = make_uint4(0, 0, 0, 0);
+      bool have_w = false;
+      if constexpr (SPEC) {                // (Spec-Raft re-arms on few events: one lane per draw)
+        if (__ballot(cinj) && cinj) {
           RS_PX(wl_px0);
           const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
           if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
@@ -646,6 +654,29 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           }
           ccount += 1;
           cnext = client_next_tick(t, d.w, S, pw);
+        }
+      } else if (!LITE) {
+        if (__ballot(cinj)) {
+          const bool cl = cinj && k == 0;
+          const bool ev = !cl && live && n.role != RAFT_LEADER && n.lid == 0 &&
+                          (n.rq.arr <= t || n.rq.c == 0);
+          if (cl || ev) {
+            RS_PX(wl_px0);
+            w = philox(sg, cl ? (uint32_t)P_CLIENT << 8 : id | P_EVENT << 8, cl ? ccount : t, 0,
+                       S.key0, S.key1);
+          }
+          have_w = ev;
+          const uint32_t dy = (uint32_t)__shfl((int)w.y, bl), dz = (uint32_t)__shfl((int)w.z, bl),
+                         dw = (uint32_t)__shfl((int)w.w, bl);
+          if (cinj) {
+            if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
+            if (1 + __umulhi(dy, N) == id) {
+              inj = true;
+              injv = dz;
+            }
+            ccount += 1;
+            cnext = client_next_tick(t, dw, S, pw);
+          }
         }
       }
       RS_PHASE(11);
@@ -686,15 +717,15 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       }
       if (live && (req_ok || res_ok || t >= n.deadline)) {
         // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready;
-        // the next timeout of a non-leader (core.clj:174) takes it when there is one, else its
-        // draw is deferred (leaders' events need none).
-        uint4 w = make_uint4(0, 0, 0, 0);
-        bool have_w = false;
+        // the next timeout of a non-leader (core.clj:174) takes it when there is one (made in P0
+        // above, or here), else its draw is deferred (leaders' events need none).
         int which = -1;
         if (req_ok && res_ok) {
-          RS_PX(wl_px2);
-          w = event_draw(sg, id, t, S);
-          have_w = true;
+          if (!have_w) {
+            RS_PX(wl_px2);
+            w = event_draw(sg, id, t, S);
+            have_w = true;
+          }
           which = (w.x & 1) ? 1 : 0;
         } else if (req_ok) {
           which = 0;
