@@ -37,6 +37,13 @@ CASES = {
     # arena pressure: arena == 2L, short logs, frequent client-sets
     "arena_tight": dict(n_clusters=512, nodes=5, seed=13, client_ppm=20000, log_cap=16,
                         arena_cap=32, dup_ppm=100000, dmax=10),
+    # arena sizes that are not a multiple of the 8-slot chunks of the arena loops (tick_wave.hpp):
+    # runs wrap inside a chunk, and chunks read past an arena's end into the next one
+    "arena_odd": dict(n_clusters=512, nodes=5, seed=14, client_ppm=20000, log_cap=16,
+                      arena_cap=37, hb=40, el_base=60, el_span=60, dup_ppm=100000, dmax=10,
+                      commit_stream_cap=5),
+    "spec_arena_odd": dict(n_clusters=512, nodes=5, seed=15, client_ppm=30000, log_cap=24,
+                           arena_cap=51, hb=40, el_base=60, el_span=60, variant_flags=2, **FAULTS),
     # launch boundaries that split ticks oddly
     "tiny_launches": dict(n_clusters=300, nodes=5, seed=17, client_ppm=1000, ticks_per_launch=7,
                           **FAULTS),
