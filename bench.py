@@ -23,8 +23,11 @@ The same JSON line carries, under "workloads", the other BASELINE configs:
             handle (the W warm-up steps run on a throwaway handle); under the faithful handlers a
             crash storm, so the line reports the live-node fraction at the window's end.
   c3_spec   the same traffic under the Spec-Raft control (SIM_SPEC §8): real replication at 1M.
-  c4_n9     config 4: 16,384 nine-node clusters per GPU, 4096-entry logs, bursty client
-            (1000+-entry AppendEntries batches, OVERFLOW halts), K steps after W warm-up steps.
+  c4_n7,    config 4: 16,384 seven- / nine-node clusters per GPU, 4096-entry logs, bursty client
+  c4_n9     (1000+-entry AppendEntries batches, OVERFLOW halts), ticks [0, 10,000 K) from
+            init-node like C3 (the replication and the halts are inside the window).
+  c4_spec   c4_n9's clusters under the Spec-Raft control: the commit index by the sorting network
+            over match_index (tick_wave.hpp).
   c5        config 5: config 3's faults and client with the vote granted without the up-to-date
             check on the Spec-Raft protocol (variant flags 3), 131,072 clusters per GPU, stepped
             1,000 ticks at a time until a safety violation is counted anywhere in the job (a MIN
@@ -50,7 +53,6 @@ Per workload:
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -59,6 +61,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path[:0] = [str(ROOT / "raft-simulation_amd"), str(ROOT / "tests"), str(ROOT / "oracle")]
+from raftsim import _build  # noqa: E402
+
+KERNEL_SOURCES = _build.KERNEL_SOURCES
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TICKS_PER_STEP = 10000
@@ -69,6 +74,16 @@ C3_DESC = ("1,048,576 five-node clusters across all GPUs x 10,000 ticks per step
            "%, delay U[1,50], partitions p=0.1 per 1000-tick epoch; client-sets in bursts (2048 of "
            "every 16384 ticks, 1 per 100 ticks on average) following up to 4 redirects; window: "
            "ticks [0, 10000 * steps) from init-node")
+C4_DESC = ("4096-entry logs, bursty client (500,000 ppm in 2048 of every 8192 ticks, up to 4 "
+           "redirects followed: 1000+-entry AppendEntries batches, OVERFLOW halts at the cap); "
+           "window: ticks [0, 10000 * steps) from init-node")
+
+
+def C4_CFG(nodes, seed):
+    return dict(nodes=nodes, seed=seed, log_cap=4096, client_ppm=500000, client_period=8192,
+                client_burst=2048, client_redirects=4)
+
+
 # name: config, clusters, per-rank scaling, window, CPU sample, description. CPU sample: (clusters,
 # steps) after a warm-up step for "steady" windows; for "init" windows cluster-steps, i.e. the
 # oracle runs cluster_steps // steps clusters over the GPU's own window from init-node.
@@ -87,12 +102,19 @@ WORKLOADS = {
                     scaling="strong", window="init", cpu=1 << 19,
                     desc="C3 under the Spec-Raft control (SIM_SPEC §8, 1024-entry logs): "
                          + C3_DESC),
-    "c4_n9": dict(cfg=dict(nodes=9, seed=5, log_cap=4096, client_ppm=500000, client_period=8192,
-                           client_burst=2048, client_redirects=4),
-                  clusters=16384, scaling="weak", window="steady", cpu=(8192, 2),
-                  desc="C4: 16,384 nine-node clusters per GPU, 4096-entry logs, bursty client "
-                       "(500,000 ppm in 2048 of every 8192 ticks, redirects followed: 1000+-entry "
-                       "AppendEntries batches, OVERFLOW halts)"),
+    # config 4 from init-node, like C3: the window holds the log growth under the bursty client,
+    # the 1000+-entry AppendEntries batches (core.clj:56-67 ships the whole suffix, log.clj:61-64)
+    # and the OVERFLOW halts at the 4096-entry cap; Spec-Raft is where the commit index comes from
+    # the sorting network over match_index
+    "c4_n7": dict(cfg=C4_CFG(7, 3), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
+                  desc="C4: 16,384 seven-node clusters per GPU, " + C4_DESC),
+    "c4_n9": dict(cfg=C4_CFG(9, 5), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
+                  desc="C4: 16,384 nine-node clusters per GPU, " + C4_DESC),
+    "c4_spec": dict(cfg=dict(C4_CFG(9, 5), variant_flags=2), clusters=16384, scaling="weak",
+                    window="init", cpu=1 << 15,
+                    desc="C4 under the Spec-Raft control (majority commit index by the sorting "
+                         "network over match_index, truncate-on-conflict): 16,384 nine-node "
+                         "clusters per GPU, " + C4_DESC),
     "c5": dict(cfg=dict(C3_CFG, variant_flags=3, log_cap=1024), clusters=131072, scaling="weak",
                window="violation", chunk=1000, max_ticks=200000,
                desc="C5: 131,072 five-node clusters per GPU with C3's faults and client, Spec-Raft "
@@ -100,10 +122,6 @@ WORKLOADS = {
                     "stepped 1,000 ticks at a time from init-node until a safety violation is "
                     "counted anywhere in the job"),
 }
-KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip",
-                  "raft-simulation_amd/csrc/steady_kernel.hip",
-                  "raft-simulation_amd/csrc/tick_wave.hpp", "raft-simulation_amd/csrc/device.hpp",
-                  "raft-simulation_amd/csrc/raftsim.hip", "include/raftsim.h"]
 HALTS = ("halt_ioobe", "halt_npe", "halt_cce", "halt_overflow")
 LIMITER = {
     "steady": "one wave per SIMD running 64 clusters' heartbeat rounds (C2 has exactly 64 clusters "
@@ -117,10 +135,8 @@ LIMITER = {
 
 
 def kernel_build_hash():
-    h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        h.update((ROOT / f).read_bytes())
-    return h.hexdigest()[:16]
+    """The hash libraftsim.so embeds (raftsim/_build.py): the kernel sources under ROOT."""
+    return _build.source_hash(ROOT)
 
 
 def window_id(spec, args):
@@ -239,6 +255,19 @@ def roofline(name, spec, count, n, launches, avg_launch_ms, delta, window, world
             "limiter": LIMITER["steady" if steady else "general"]}
 
 
+def survey_8d(rate, n, delta):
+    """SURVEY §8(d)'s per-node-tick accounting, B(N) = 2(32 + 8N) + 8 + 64 m + 16 e bytes per
+    simulated node-tick, priced at the line's rate: a 'fraction' above 1 means the kernels never
+    touch most node-ticks (idle ticks are skipped exactly, fixed-point rounds fold into hashes),
+    so it measures the algorithm, not the memory system; `frac` (compulsory bytes per launch over
+    the launch time) is the physical fraction."""
+    nt = max(1, delta["node_ticks"])
+    b = 2 * (32 + 8 * n) + 8 + 64 * delta["delivered"] / nt + 16 * delta["entries_appended"] / nt
+    return {"bytes_per_node_tick": b, "value": rate * b / (HBM_PEAK_GBS * 1e9),
+            "note": "SURVEY 8(d) rate x B / 8e12; not a bandwidth fraction here (idle node-ticks "
+                    "are skipped exactly, so it exceeds 1): see frac"}
+
+
 def run_workload(name, args, world, rank, local_rank, dist):
     import raftsim
     from raftsim import dist as rdist
@@ -277,8 +306,10 @@ def run_workload(name, args, world, rank, local_rank, dist):
             w.step(TICKS_PER_STEP)
         w.sync()
         w.close()
-    sims = [make()] if kind != "first" else []
-    sim = sims[0] if sims else None
+    # config 2 as named: a fresh handle per repetition, created (alloc + init-node kernel) before
+    # the timed region; each repetition is one 10k-tick step from init-node
+    sims = [make() for _ in range(spec["reps"])] if kind == "first" else [make()]
+    sim = sims[0] if kind != "first" else None
     if kind == "steady":
         for _ in range(args.warmup):
             sim.step(TICKS_PER_STEP)
@@ -290,13 +321,12 @@ def run_workload(name, args, world, rank, local_rank, dist):
     t0 = time.perf_counter()
     span_ms, kernel_ms, launches = 0.0, 0.0, 0
     if kind == "first":
-        # config 2 as named: a fresh handle per repetition, one 10k-tick step from init-node
-        reps = spec["reps"]
         c_sum = None
-        for _ in range(reps):
-            s = make()
+        for s in sims:
             s.step_async(TICKS_PER_STEP)
             s.sync()
+        wall_first = time.perf_counter() - t0
+        for s in sims:
             span_ms += s.last_span()
             ms, nl = s.last_step_timing()
             kernel_ms += ms * nl
@@ -305,8 +335,7 @@ def run_workload(name, args, world, rank, local_rank, dist):
             c_sum = c if c_sum is None else {k: (c_sum[k] + c[k]) if isinstance(c[k], int) and
                                              k not in ("first_violation_tick", "payload_max")
                                              else c[k] for k in c}
-            s.close()
-        steps = reps
+        steps = len(sims)
     elif kind == "init":
         # one sync per step: the live-node count after every step (halts are permanent, so the
         # halt counters count the halted nodes); the device time of each step is its own span
@@ -330,16 +359,22 @@ def run_workload(name, args, world, rank, local_rank, dist):
         kernel_ms = ms * launches
     barrier()
     wall = time.perf_counter() - t0
+    if kind == "first":
+        wall = wall_first          # the counter reads after the steps are not the steps' time
     avg_launch_ms = kernel_ms / max(1, launches)
-    launch_src = "HIP events in the launches' dispatch packets, averaged over the timed launches"
+    timed = sim.timed_launches() if sim is not None else launches
+    launch_src = (f"HIP events in the launches' dispatch packets, averaged over the {timed} timed "
+                  f"launches")
     if kind == "steady" and steps:
         # A steady window is one dispatch per step, and only the first launch after the sync
-        # carries events (an event pair costs ~6 us per dispatch): the device span per step bounds
-        # the average launch from above, and one timed launch is a sample of one.
-        if span_ms / steps < avg_launch_ms:
-            avg_launch_ms = span_ms / steps
-            launch_src = ("device span / steps (one dispatch per step; bounds the average launch "
-                          "from above, below the one timed launch)")
+        # carries events (an event pair costs ~6 us per dispatch): one timed launch is a sample of
+        # one, so the roofline takes the device span per step, which bounds the average launch
+        # from above (it adds the gaps between back-to-back launches)
+        extra["timed_launch_ms"] = avg_launch_ms
+        extra["timed_launches"] = timed
+        avg_launch_ms = span_ms / steps
+        launch_src = ("device span / steps: one dispatch per step, so this bounds the average "
+                      f"launch from above (the {timed} event-timed launch: timed_launch_ms)")
     if kind == "first":
         delta = {k: v for k, v in c_sum.items()}
         live = [nodes, nodes - sum(c_sum[h] for h in HALTS) // max(1, spec["reps"])]
@@ -383,9 +418,12 @@ def run_workload(name, args, world, rank, local_rank, dist):
         "live_node_frac_end": live_end / (total * n),
         "live_node_ticks_per_s": live_ticks / (span_max * 1e-3),
         "payload_evicted": delta["payload_evicted"],
+        "ev_ae": delta["ev_ae"],
+        "payload_max": delta["payload_max"],
         "counters": {k: v for k, v in delta.items() if v},
         **extra,
     }
+    rec["roofline"]["survey_8d"] = survey_8d(rec["value"], n, delta)
     if kind == "first":
         rec["reps"] = spec["reps"]
     if delta["payload_evicted"]:
@@ -436,6 +474,7 @@ def run_violation(name, spec, args, world, rank, dist, make, count, total, offse
         "roofline": roofline(name, spec, count, n, launches, avg_launch_ms, c, window, world),
         "counters": {k: v for k, v in c.items() if v},
     }
+    rec["roofline"]["survey_8d"] = survey_8d(rec["value"], n, c)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import helpers
 
@@ -462,8 +501,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2+c2_init+c3+c3_spec+c4_n9+c5",
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2+c2_init+c3+c3_spec+c4_n7+c4_n9+c4_spec+c5",
                     help="headline[+extra...] from " + ", ".join(WORKLOADS))
     ap.add_argument("--clusters", type=int, default=0, help="override the headline's clusters")
     ap.add_argument("--no-cpu-baseline", action="store_true")

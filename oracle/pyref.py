@@ -770,8 +770,9 @@ class PyCluster:
         src = msg_src(msg) if msg is not None else 0
         mterm = msg.get("term", 0) if msg is not None else 0
         # two 64-bit words: (t, ev | src << 3 | role << 7 | fault << 9), (msg_term, current_term)
+        # (the C oracle and the kernels take t, msg_term and current_term as uint32: mask alike)
         small = ev | src << 3 | ROLE_CODE[node["state"]] << 7 | fault << 9
-        return [t | small << 32, mterm | node["current-term"] << 32]
+        return [(t & M32) | small << 32, (mterm & M32) | (node["current-term"] & M32) << 32]
 
     def _violation(self, kind, t):
         self.cnt[kind] += 1

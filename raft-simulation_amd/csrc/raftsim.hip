@@ -57,6 +57,7 @@ struct Shard {
   DevSim d;
   std::vector<void*> allocs;
   double last_ms, last_step_ms;
+  uint32_t last_timed;           // launches of the last sync window that carried an event pair
   bool pending;                  // launches enqueued since the last sync
   uint32_t pending_launches;
   uint32_t last_launches;
@@ -405,7 +406,8 @@ static int sh_sync(Shard* s) {
     kms += one;
     ++timed;
   }
-  s->last_ms = timed ? kms / timed : 0.0;         // per tick-kernel launch
+  s->last_ms = timed ? kms / timed : 0.0;         // per timed tick-kernel launch
+  s->last_timed = timed;
   s->last_step_ms = ms;                           // + the schedule's key and sort kernels
   s->last_launches = launches;
   return 0;
@@ -1009,6 +1011,25 @@ int raft_sim_read_counters(raft_sim_t* r, raft_counters_t* out) {
     out->payload_max = std::max(out->payload_max, c.payload_max);
   }
   return 0;
+}
+
+// Build identity (not part of include/raftsim.h): the hash of the kernel sources this library was
+// compiled from (raftsim/_build.py; __graft_entry__.build_lib passes it), also findable in the
+// file's bytes as "RAFTSIM_SRC_HASH=<hash>" without loading it.
+#ifndef RAFTSIM_SRC_HASH
+#define RAFTSIM_SRC_HASH "unknown"
+#endif
+static const char g_src_tag[] = "RAFTSIM_SRC_HASH=" RAFTSIM_SRC_HASH;
+extern "C" const char* raftsim_src_hash(void) { return g_src_tag + 17; }
+
+// Diagnostic (not part of include/raftsim.h): how many launches of the last sync window the
+// average of raft_sim_last_step_timing is taken over (every general launch; the first steady
+// launch after a sync), summed over shards.
+extern "C" int raftsim_last_timed_launches(raft_sim_t* r) {
+  if (!r) return fail(-EINVAL, "null sim");
+  int n = 0;
+  for (Shard* s : r->sh) n += (int)s->last_timed;
+  return n;
 }
 
 // Diagnostic (not part of include/raftsim.h): clusters the steady kernel handed to the catch-up

@@ -109,32 +109,28 @@ __device__ __forceinline__ void trace_record(const DevSim& S, uint32_t gi, uint3
 // arena, or the ARENA_PAD_SLOTS of padding after the last one (raftsim.hip); those lanes of the
 // chunk are masked.
 
-// Log Matching over cnt consecutive positions of two logs whose first slots are xi in arena xa
-// and yi in arena ya: is there a position with the same term and a different value?
+// One chunk of a Log Matching run: compares up to W consecutive positions of two logs whose next
+// slots are xi in arena xa and yi in arena ya (cnt positions left in the run). Returns the
+// positions consumed (the chunk ends at the run's end or at either arena's wrap point) and sets
+// hit when one of them has the same term and a different value. The caller advances xi / yi
+// (wrapping at A) and loops; the checker (P4) interleaves these steps over a wave's lanes.
 template <int W = 8>
-__device__ __forceinline__ bool log_conflict(const uint2* xa, uint32_t xi, const uint2* ya,
-                                             uint32_t yi, uint32_t cnt, uint32_t A) {
-  while (cnt) {
-    const uint32_t c = min(min(cnt, (uint32_t)W), min(A - xi, A - yi));
-    const uint2* xp = xa + xi;
-    const uint2* yp = ya + yi;
-    uint2 x[W], y[W];
+__device__ __forceinline__ uint32_t log_conflict_chunk(const uint2* xa, uint32_t xi,
+                                                       const uint2* ya, uint32_t yi, uint32_t cnt,
+                                                       uint32_t A, bool& hit) {
+  const uint32_t c = min(min(cnt, (uint32_t)W), min(A - xi, A - yi));
+  const uint2* xp = xa + xi;
+  const uint2* yp = ya + yi;
+  uint2 x[W], y[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      x[j] = xp[j];
-      y[j] = yp[j];
-    }
-    bool hit = false;
-#pragma unroll
-    for (int j = 0; j < W; ++j) hit |= (uint32_t)j < c && x[j].x == y[j].x && x[j].y != y[j].y;
-    if (hit) return true;
-    cnt -= c;
-    xi += c;
-    yi += c;
-    xi = xi == A ? 0 : xi;
-    yi = yi == A ? 0 : yi;
+  for (int j = 0; j < W; ++j) {
+    x[j] = xp[j];
+    y[j] = yp[j];
   }
-  return false;
+  hit = false;
+#pragma unroll
+  for (int j = 0; j < W; ++j) hit |= (uint32_t)j < c && x[j].x == y[j].x && x[j].y != y[j].y;
+  return c;
 }
 
 // Copy `cnt` arena entries from slot si of `src` to slot di of `dst`, in ascending order with every
@@ -1279,19 +1275,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               cur = (uint32_t)a;
             }
             if (rem) {
-              const uint32_t c = min(min(rem, (uint32_t)W), min(A - xi, A - yi));
-              const uint2* xp = xa + xi;
-              const uint2* yp = sar + yi;
-              uint2 x[W], y[W];
-  #pragma unroll
-              for (int j = 0; j < W; ++j) {
-                x[j] = xp[j];
-                y[j] = yp[j];
-              }
-              bool hit = false;
-  #pragma unroll
-              for (int j = 0; j < W; ++j)
-                hit |= (uint32_t)j < c && x[j].x == y[j].x && x[j].y != y[j].y;
+              bool hit;
+              const uint32_t c = log_conflict_chunk<W>(xa, xi, sar, yi, rem, A, hit);
               if (hit) {
                 found |= 1u << cur;
                 rem = 0;

@@ -1,5 +1,5 @@
 """Device time per C2 step of the library builds given (diagnostic): the normal build and probe
-builds (-DRS_PROBE_LOADONLY: the steady dispatch returns after its state load). Usage:
+builds (e.g. -DRS_WAVELOG, built by scripts/build_variants.sh). Usage:
 dispatch_probe.py LIB [LIB ...]"""
 import sys
 from pathlib import Path

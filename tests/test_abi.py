@@ -34,6 +34,19 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, sym)
 
 
+def test_library_is_built_from_these_sources():
+    """libraftsim.so embeds the hash of the kernel sources it was compiled from; it must be this
+    tree's (a stale binary would ship to the GPU box beside newer sources, and Simulator refuses
+    it there). build_lib() rebuilds on a mismatch."""
+    from raftsim import _build
+
+    assert raftsim.LIB_PATH.exists(), "run __graft_entry__.build() first"
+    assert _build.embedded_hash(raftsim.LIB_PATH) == _build.source_hash()
+    lib = ctypes.CDLL(str(raftsim.LIB_PATH))
+    lib.raftsim_src_hash.restype = ctypes.c_char_p
+    assert lib.raftsim_src_hash().decode() == _build.source_hash()
+
+
 def test_oracle_mirrors_the_abi():
     import helpers
     lib = ctypes.CDLL(str(helpers.ORACLE_LIB))

@@ -29,12 +29,18 @@ def test_default_workloads_cover_the_baseline_configs(bench):
     assert default is not None
     names = default.split("+")
     assert names[0] == "c2"                      # the headline line is config 2
-    assert {"c2", "c2_init", "c3", "c3_spec", "c4_n9", "c5"} <= set(names)
+    assert {"c2", "c2_init", "c3", "c3_spec", "c4_n7", "c4_n9", "c4_spec", "c5"} <= set(names)
     assert all(n in bench.WORKLOADS for n in names)
     w = bench.WORKLOADS
     assert w["c2"]["clusters"] == 65536 and w["c2"]["cfg"]["nodes"] == 5
     assert w["c3"]["clusters"] == 1 << 20 and w["c3"]["cfg"]["drop_ppm"] == 100000
-    assert w["c4_n9"]["cfg"]["nodes"] == 9 and w["c4_n9"]["cfg"]["log_cap"] == 4096
+    # config 4: 7- and 9-node clusters with 4096-entry logs, from init-node (the replication
+    # and its 1000+-entry AppendEntries are inside the window), and its Spec-Raft form (the
+    # commit index by the sorting network)
+    for name, nodes in (("c4_n7", 7), ("c4_n9", 9), ("c4_spec", 9)):
+        assert w[name]["cfg"]["nodes"] == nodes and w[name]["cfg"]["log_cap"] == 4096
+        assert w[name]["window"] == "init"
+    assert w["c4_spec"]["cfg"]["variant_flags"] == 2
     assert w["c5"]["cfg"]["variant_flags"] & 1 and w["c5"]["window"] == "violation"
 
 
@@ -51,6 +57,21 @@ def test_roofline_is_compulsory_bytes_over_launch_time(bench):
     assert r["frac_event_model"] > r["frac"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s"
     assert r["traffic"] is None                       # no profile of window "none"
+
+
+def test_default_warmup_is_the_drivers(bench):
+    """The driver runs `bench.py --steps 20 --warmup 5`: the defaults are that window, so the
+    PMC profiles taken with the defaults describe the driver's window."""
+    src = (ROOT / "bench.py").read_text()
+    assert 'ap.add_argument("--warmup", type=int, default=5)' in src
+    assert 'ap.add_argument("--steps", type=int, default=20)' in src
+
+
+def test_survey_8d_accounting(bench):
+    d = {"node_ticks": 10 ** 9, "delivered": 0, "entries_appended": 0}
+    r = bench.survey_8d(1e14, 5, d)
+    assert r["bytes_per_node_tick"] == 152                  # BASELINE.md: B(5) with m = e = 0
+    assert r["value"] == pytest.approx(1e14 * 152 / 8e12)
 
 
 def test_windows(bench):

@@ -260,3 +260,14 @@ def test_client_gap_without_client_rate():
     assert r.counters()["client_injected"] == 8
     assert all(c["client_next"] == 0xFFFFFFFF for c in r.read_clusters())
     assert pyref.client_gap(12345, pyref.client_powers(0)) == 2 ** 32 - 1
+
+
+def test_trace_words_are_u32_like_the_c_oracle():
+    """The trace-hash words take t, msg_term and current_term as uint32, as raftref.c and the
+    kernels do (SIM_SPEC §4): a term at or past 2^32 contributes its low 32 bits only."""
+    pc = pyref.PyCluster(pyref.default_config(), 0)
+    node = dict(pyref.init_node(1), **{"current-term": (1 << 32) + 5})
+    msg = {"type": "append-entries", "term": (1 << 33) + 7, "leader-id": 2}
+    lo, hi = pc._trace_words((1 << 32) + 9, 2, msg, node, 0)
+    assert lo & 0xFFFFFFFF == 9 and hi == 7 | 5 << 32
+    assert max(lo, hi) < 1 << 64
