@@ -48,12 +48,43 @@ __device__ __forceinline__ uint32_t msel(bool a, uint32_t x, uint32_t y) {
   return (x & m) | (y & ~m);
 }
 
-// Dynamic LDS of a steady workgroup: one tick_wave LDS block for the catch-up, which the
-// workgroup's first wave runs alone (hand-overs are rare where the steady path is taken, and four
-// blocks' LDS measured +0.8 us on every dispatch's launch).
+// The state image. A wave stages its 64 clusters' blocks (the first IMG_SLOTS 16-B chunks of each:
+// four 128-B lines at N >= 4) in LDS: loads and stores then move whole lines, eight lines per wave
+// instruction, where a lane reading its own cluster's block straight into registers touches 64
+// lines per instruction (one per lane, the texture path's rate) -- the load phase's cost.
+// Chunk i of the wave's cluster l sits in slot i ^ (l & 15) of l's 512-B row: the LDS-DMA loads
+// (global_load_lds: lane-linear destination) take the swizzle on their source addresses, and a
+// lane reading chunk i of its own cluster, or writing it back, meets no bank conflict (the 16 lanes
+// of a ds_read_b128 group have distinct l & 15).
+constexpr int IMG_SLOTS = 32;                               // slots per cluster row
+constexpr uint32_t IMG_ROW = IMG_SLOTS * 16;                // bytes
+constexpr uint32_t IMG_WAVE = 64 * IMG_ROW;                 // 32 KiB per wave
+__device__ __forceinline__ uint32_t img_off(uint32_t l, uint32_t i) {
+  return l * IMG_ROW + 16u * (i ^ (l & 15u));
+}
+template <typename T>
+__device__ __forceinline__ T* lds_at(char* img, uint32_t off) {
+  return reinterpret_cast<T*>(img + off);
+}
+
+// Dynamic LDS of a steady workgroup: the four waves' state images. A wave that bailed clusters
+// runs them through the general tick body with its own image as that body's LDS block (the image
+// is dead once the write-back has read it): the waves of a workgroup never wait for each other.
 template <int N>
 constexpr size_t steady_lds_bytes() {
-  return block_lds_bytes<N, false>();
+  static_assert(block_lds_bytes<N, false>() <= IMG_WAVE, "the catch-up block fits a wave's image");
+  return 4 * (size_t)IMG_WAVE;
+}
+
+// Wave-wide sum (all 64 lanes active), uniform: DPP row shifts and broadcasts as in wave_min.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return __builtin_amdgcn_readlane(x, 63);
 }
 
 template <int N>
@@ -62,14 +93,14 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   constexpr int F = N - 1;
   constexpr uint32_t HB = hot_block_words(N), CLW = hot_cl_off(N);
   // the words read: the cluster's (checker hwm) and every node field up to the leader-state rows
-  // (device.hpp: words 0-122 at N = 5, four lines), loaded at once -- the leader's rows are picked
-  // from them once its id is known, with no second round trip
+  // (device.hpp: words 0-122 at N = 5, four lines) -- the leader's rows are picked from them once
+  // its id is known, with no second round trip. The image holds whole lines of the block.
   constexpr int NWORDS = (int)(HOT_CW + hf_abase(N) * N);
   constexpr int NW4 = (NWORDS + 3) / 4;
+  constexpr int IMGC = (int)(HB / 4) < IMG_SLOTS ? (int)(HB / 4) : IMG_SLOTS;   // chunks staged
+  static_assert(NW4 <= IMGC && IMGC % 8 == 0, "the image holds the words read, in whole lines");
   static_assert(CLW == 0, "the cluster words lead the block");
-  __shared__ uint32_t sctr[4];
-  __shared__ uint32_t nbl;                         // clusters this workgroup bailed
-  __shared__ uint32_t bl_c[LANE_WG], bl_t[LANE_WG];   // bailed cluster, tick it stopped before
+  __shared__ uint32_t bl_c[LANE_WG], bl_t[LANE_WG];   // per wave: bailed cluster, tick it stopped before
   extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // the previous steady launch's bail count (complete: that launch has ended) to the host, which
@@ -80,16 +111,27 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     if (S.bail_report && prev) *S.bail_report = prev;
     if (prev) *S.nbail_zero = 0;
   }
-  if (threadIdx.x < 4) sctr[threadIdx.x] = 0;
-  if (threadIdx.x == 0) nbl = 0;
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t c0 = blockIdx.x * LANE_WG + threadIdx.x < S.C ? blockIdx.x * LANE_WG + threadIdx.x
-                                                                 : INF;   // clusters in id order
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t cbase = blockIdx.x * LANE_WG + wave * 64;      // the wave's clusters, in id order
+  const uint32_t c0 = cbase + lane < S.C ? cbase + lane : INF;
   const bool active = c0 != INF;
   const uint32_t c = active ? c0 : 0u;
   const uint32_t g = S.goff + c;
-  uint32_t* const blk = S.hot + (size_t)c * HB;
+  char* const img = reinterpret_cast<char*>(dsm) + wave * IMG_WAVE;
+  uint32_t* const blc = bl_c + wave * 64;
+  uint32_t* const blt = bl_t + wave * 64;
+  uint32_t nbw = 0;                                   // clusters this wave bailed (uniform)
+  // a compaction point: every lane of the wave active
+  auto record_bail = [&](bool b, uint32_t tick) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+    if (b) {
+      const uint32_t i = nbw + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      blc[i] = c;
+      blt[i] = tick;
+    }
+    nbw += (uint32_t)__popcll(m);
+  };
 #ifdef RS_WAVELOG   // diagnostic build: per-wave timeline (scripts/lane_timeline.py)
   const uint64_t wl_start = wall_clock64();
   uint32_t wl_trips = 0, wl_first = 0, wl_ph[6] = {0, 0, 0, 0, 0, 0};
@@ -104,17 +146,30 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #define RS_LPH(i) do {} while (0)
 #endif
 
-  // ------------------------------------------- load: the checker hwm and fields up to the rows
-  uint32_t w[NW4 * 4];
+  // ------------------------------------------- load: the wave's blocks into its image (LDS-DMA)
+  {
+    const uint32_t p = lane & 31;
 #pragma unroll
-  for (int i = 0; i < NW4 * 4; ++i) w[i] = 0;
-  if (active) {
-#pragma unroll
-    for (int i = 0; i < NW4; ++i) {
-      const uint4 x = reinterpret_cast<const uint4*>(blk)[i];
-      w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+    for (int j = 0; j < 32; ++j) {                  // clusters 2j, 2j + 1: 32 slots each
+      const uint32_t cc = 2 * j + (lane >> 5);
+      const uint32_t i = p ^ (cc & 15u);
+      const uint32_t cg = min(cbase + cc, S.C - 1);  // past the shard's end: any block, unused
+      if (i < (uint32_t)IMGC)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(S.hot + (size_t)cg * HB + 4 * i),
+            (__attribute__((address_space(3))) void*)(img + j * 1024), 16, 0, 0);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's own LDS-DMA writes have landed
+  uint32_t w[NW4 * 4];
+#pragma unroll
+  for (int i = 0; i < NW4; ++i) {
+    const uint4 x = *lds_at<const uint4>(img, img_off(lane, i));
+    w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+  }
+#ifdef RS_WAVELOG
+  wl_loop = wall_clock64();
+#endif
   auto field = [&](int f, uint32_t (&out)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) out[k] = w[HOT_CW + f * N + k];
@@ -215,47 +270,73 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     const uint32_t Lqm = pick<N>(nqm, L);
     bad = (Lqm >> 4) & 31;                                   // the leader's REQ queue is empty
     const uint32_t rsh = (Lqm >> 9) & 15, rsc = (Lqm >> 13) & 31;
+    uint32_t need = 0, rqh[F];
 #pragma unroll
     for (int j = 0; j < F; ++j) {
       const uint32_t qm = fsel(nqm, j);
-      const uint32_t rqh = qm & 15, rqc = (qm >> 4) & 31;
+      const uint32_t rqc = (qm >> 4) & 31;
+      rqh[j] = qm & 15;
       bad = bad || rqc > 1 || ((qm >> 13) & 31) != 0;       // <= 1 request, no responses
-      if (!bad && rqc) {                                    // the leader's append-entries
-        const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, c * N + fk(j), 0) +
-                                                         rqh * qstride(S, 0));
-        const uint4 m0 = mp[0], m1 = mp[1];
-        bad = m0.y != (RAFT_MSG_APPEND_ENTRIES | Lid << 3) || m1.y || m1.z || m1.w;
-        qmask |= 1u << j;
-        qA[j] = m0.x; qT[j] = m0.z; qa[j] = m0.w; qb[j] = m1.x;
-      }
+      need |= (uint32_t)(rqc != 0) << j;
     }
     bad = bad || rsc > (uint32_t)F;
-    uint32_t last = 0;
-    for (uint32_t i = 0; i < rsc && !bad; ++i) {            // append-responses, sender order
-      const uint4* mp = reinterpret_cast<const uint4*>(qslots(S, c * N + L, 1) +
-                                                       wrapq(rsh + i, S.Q) * qstride(S, 1));
-      const uint4 m0 = mp[0], m1 = mp[1];
-      const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
-      bad = (hdr & 7) != RAFT_MSG_APPEND_RESPONSE || (hdr >> 8) || m1.y || m1.z || m1.w ||
-            src <= last || src > (uint32_t)N || src == Lid || (i && m0.x != resA);
-      last = src;
-      resA = m0.x;
-      const uint32_t j = src - 1 - (src > Lid ? 1u : 0u);
-      rmask |= 1u << j;
+    // The messages: loaded by every lane of a wave in which any lane has one (a message in flight
+    // at the launch's start is rare), all loads issued before any is looked at -- one memory round
+    // trip, where loads under per-lane branches each waited for the last. Slot indices are
+    // clamped into the ring for lanes whose queue words are not looked at.
+    uint4 qm0[F], qm1[F], rm0[F], rm1[F];
+    if (__builtin_amdgcn_ballot_w64(!bad && (need || rsc))) {     // wave-uniform
 #pragma unroll
-      for (int jj = 0; jj < F; ++jj) {
-        if ((uint32_t)jj == j) {
-          rT[jj] = m0.z; rA[jj] = m0.w; rB[jj] = m1.x; rH[jj] = (hdr >> 7) & 1;
+      for (int j = 0; j < F; ++j) {                          // the leader's append-entries
+        const uint4* mp = reinterpret_cast<const uint4*>(
+            qslots(S, c * N + fk(j), 0) + min(rqh[j], S.Q - 1) * qstride(S, 0));
+        qm0[j] = mp[0];
+        qm1[j] = mp[1];
+      }
+#pragma unroll
+      for (int i = 0; i < F; ++i) {                          // append-responses, sender order
+        const uint4* mp = reinterpret_cast<const uint4*>(
+            qslots(S, c * N + L, 1) + min(wrapq(rsh + i, S.Q), S.Q - 1) * qstride(S, 1));
+        rm0[i] = mp[0];
+        rm1[i] = mp[1];
+      }
+    }
+    if (!bad) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if ((need >> j) & 1) {
+          const uint4 m0 = qm0[j], m1 = qm1[j];
+          bad = bad || m0.y != (RAFT_MSG_APPEND_ENTRIES | Lid << 3) || m1.y || m1.z || m1.w;
+          qmask |= 1u << j;
+          qA[j] = m0.x; qT[j] = m0.z; qa[j] = m0.w; qb[j] = m1.x;
+        }
+      }
+      uint32_t last = 0;
+#pragma unroll
+      for (int i = 0; i < F; ++i) {
+        if ((uint32_t)i < rsc && !bad) {
+          const uint4 m0 = rm0[i], m1 = rm1[i];
+          const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
+          bad = (hdr & 7) != RAFT_MSG_APPEND_RESPONSE || (hdr >> 8) || m1.y || m1.z || m1.w ||
+                src <= last || src > (uint32_t)N || src == Lid || (i && m0.x != resA);
+          last = src;
+          resA = m0.x;
+          const uint32_t j = src - 1 - (src > Lid ? 1u : 0u);
+          if (!bad) {
+            rmask |= 1u << j;
+#pragma unroll
+            for (int jj = 0; jj < F; ++jj) {
+              if ((uint32_t)jj == j) {
+                rT[jj] = m0.z; rA[jj] = m0.w; rB[jj] = m1.x; rH[jj] = (hdr >> 7) & 1;
+              }
+            }
+          }
         }
       }
     }
     if (!rmask) resA = INF;
   }
-  if (active && bad) {                      // outside the model from the start: bail at t0
-    const uint32_t i = atomicAdd(&nbl, 1u);
-    bl_c[i] = c;
-    bl_t[i] = t0;
-  }
+  record_bail(active && bad, t0);           // outside the model from the start: bail at t0
   const bool wb = active && !bad;
   bool run = wb;
 
@@ -281,10 +362,13 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     return m;
   };
 #ifdef RS_WAVELOG
-  wl_loop = wall_clock64();
   wl_ts = __builtin_amdgcn_s_memtime();
 #endif
+  bool pbail = false;                        // bailed in the last trip, not yet recorded
+  uint32_t pbt = 0;
   for (;;) {
+    record_bail(pbail, pbt);                 // the loop's head: every lane active
+    pbail = false;
     uint32_t t = max(tn, next_event());
     // a deferred deadline at or before the tick to decide is drawn first (it can only move later)
     for (;;) {
@@ -343,9 +427,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
     RS_LPH(1);
     if (bail) {                              // the general tick body runs this tick
-      const uint32_t i = atomicAdd(&nbl, 1u);
-      bl_c[i] = c;
-      bl_t[i] = t;
+      pbail = true;
+      pbt = t;
       run = false;
       continue;
     }
@@ -520,6 +603,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       pend &= ~same;
     }
   }
+  uint32_t dl = 0;                           // lines of the cluster's block changed
   if (wb) {
     // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
     constexpr int NV = HF_NEXT;
@@ -552,31 +636,35 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
     auto live = [](int q) { return q >= (int)HOT_CW && q < (int)(HOT_CW + HF_NEXT * N); };
     auto val = [&](int q) { return v[(q - HOT_CW) / N][(q - HOT_CW) % N]; };
-    // Only words that changed are stored (in a heartbeat round the deadlines and trace hashes do,
-    // all in the block's first line; flags, terms, masks, commits, queue words and rows come back
-    // unchanged): a lane's stores each go to a different cluster's block, and every dirty line is
-    // written back at the launch end.
+    // The changed chunks into the image (in a heartbeat round the deadlines and trace hashes
+    // change, all in the block's first line; flags, terms, masks, commits, queue words and rows
+    // come back unchanged); the lines they dirty go back to memory whole, below.
 #pragma unroll
     for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_NEXT * N + 3) / 4; ++i) {
-      const int lo = 4 * i;
-      if (live(lo) && live(lo + 1) && live(lo + 2) && live(lo + 3)) {
-        if (val(lo) != w[lo] || val(lo + 1) != w[lo + 1] || val(lo + 2) != w[lo + 2] ||
-            val(lo + 3) != w[lo + 3])
-          reinterpret_cast<uint4*>(blk)[i] =
-              make_uint4(val(lo), val(lo + 1), val(lo + 2), val(lo + 3));
-      } else {
-#pragma unroll
-        for (int q = lo; q < lo + 4; ++q)
-          if (live(q) && val(q) != w[q]) blk[q] = val(q);
+      const int q = 4 * i;
+      const uint4 x = make_uint4(live(q) ? val(q) : w[q], live(q + 1) ? val(q + 1) : w[q + 1],
+                                 live(q + 2) ? val(q + 2) : w[q + 2],
+                                 live(q + 3) ? val(q + 3) : w[q + 3]);
+      if (x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3]) {
+        *lds_at<uint4>(img, img_off(lane, i)) = x;
+        dl |= 1u << (i / 8);
       }
     }
     // the leader's rows (node L): next / match of peer fk(j) + 1
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      if (nx[j] != nx0[j]) blk[HOT_CW + (HF_NEXT + fk(j)) * N + L] = (uint32_t)nx[j];
-      if (mt[j] != mt0[j]) blk[HOT_CW + (HF_NEXT + N + fk(j)) * N + L] = (uint32_t)mt[j];
+      const uint32_t qn = HOT_CW + (HF_NEXT + fk(j)) * N + L;
+      const uint32_t qt = HOT_CW + (HF_NEXT + N + fk(j)) * N + L;
+      if (nx[j] != nx0[j]) {
+        *lds_at<uint32_t>(img, img_off(lane, qn / 4) + 4 * (qn % 4)) = (uint32_t)nx[j];
+        dl |= 1u << (qn / 32);
+      }
+      if (mt[j] != mt0[j]) {
+        *lds_at<uint32_t>(img, img_off(lane, qt / 4) + 4 * (qt % 4)) = (uint32_t)mt[j];
+        dl |= 1u << (qt / 32);
+      }
     }
-    // queues back to the rings, heads at slot 0
+    // queues back to the rings, heads at slot 0 (a message in flight at the launch's end: rare)
 #pragma unroll
     for (int j = 0; j < F; ++j) {
       if ((qmask >> j) & 1) {
@@ -598,15 +686,30 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       }
     }
   }
+  // Dirty lines back to memory whole: a wave instruction writes eight clusters' line (8 lanes x
+  // 16 B each), read from the image (line ln of cluster cc is its chunks 8 ln .. 8 ln + 7).
+#pragma unroll
+  for (int ln = 0; ln < IMGC / 8; ++ln) {
+    const uint64_t bal = __builtin_amdgcn_ballot_w64((dl >> ln) & 1);
+    if (!bal) continue;                                  // wave-uniform
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+      const uint32_t cc = 8 * gq + (lane >> 3), q = 8 * ln + (lane & 7);
+      if ((bal >> cc) & 1) {
+        const uint4 x = *lds_at<const uint4>(img, img_off(cc, q));
+        *reinterpret_cast<uint4*>(S.hot + (size_t)(cbase + cc) * HB + 4 * q) = x;
+      }
+    }
+  }
 #ifdef RS_WAVELOG
   {
     const uint64_t wl_end = wall_clock64();
     const uint32_t emax = ~wave_min(~wl_events), emin = wave_min(wl_events);
-    if ((threadIdx.x & 63) == 0 && S.wavelog) {
+    if (lane == 0 && S.wavelog) {
       uint32_t hw, xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)(blockIdx.x * 4 + threadIdx.x / 64) * 32);
+      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)(blockIdx.x * 4 + wave) * 32);
       rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
                           (uint32_t)(wl_end >> 32));
       rec[1] = make_uint4(wl_trips, hw, xcc, wl_first);
@@ -616,39 +719,41 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
   }
 #endif
-  // counters: heartbeats, append-entries, append-responses; every message is delivered
-  if (nhb) atomicAdd(&sctr[0], nhb);
-  if (nae) atomicAdd(&sctr[1], nae);
-  if (nar) atomicAdd(&sctr[2], nar);
-  // the bailed clusters' words are this workgroup's own stores: its waves see them after the
-  // barrier (same CU; no other workgroup reads them in this launch)
-  __syncthreads();
-  unsigned long long* const ctr = S.ctr + (size_t)(blockIdx.x % CTR_COPIES) * CTR_STRIDE;
-  if (threadIdx.x < 5) {
-    const uint32_t h = sctr[0], a = sctr[1], r = sctr[2];
-    const uint32_t msgs = (uint32_t)F * h + a;
-    const uint32_t x = threadIdx.x;
-    const int idx = x == 0 ? RAFT_CTR_EV_HEARTBEAT : x == 1 ? RAFT_CTR_EV_AE
-                  : x == 2 ? RAFT_CTR_EV_AR : x == 3 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
-    const uint32_t v = x == 0 ? h : x == 1 ? a : x == 2 ? r : msgs;
-    if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
+  // counters: heartbeats, append-entries, append-responses; every message is delivered. One
+  // wave-wide sum each, added by five lanes to the wave's copy of the counter block.
+  {
+    const uint32_t h = wave_sum(nhb), a = wave_sum(nae), r = wave_sum(nar);
+    unsigned long long* const ctr =
+        S.ctr + (size_t)((blockIdx.x * 4 + wave) % CTR_COPIES) * CTR_STRIDE;
+    if (lane < 5) {
+      const uint32_t msgs = (uint32_t)F * h + a;
+      const int idx = lane == 0 ? RAFT_CTR_EV_HEARTBEAT : lane == 1 ? RAFT_CTR_EV_AE
+                    : lane == 2 ? RAFT_CTR_EV_AR : lane == 3 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
+      const uint32_t v = lane == 0 ? h : lane == 1 ? a : lane == 2 ? r : msgs;
+      if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
+    }
   }
   // ---------------------------------------------------------------- catch-up
-  // The bailed clusters, each from the tick it stopped before to the launch's end, through the
-  // general tick body: the workgroup's first wave takes the list's wave slots in turn.
-  const uint32_t nb = nbl;
-#ifdef RS_WAVELOG   // the workgroup's end: its stores drained (the barrier's release) and counted
-  if (threadIdx.x == 0 && S.wavelog) {
+  // The wave's bailed clusters, each from the tick it stopped before to the launch's end, through
+  // the general tick body, with the wave's image as its LDS block (the write-back above read the
+  // image: a wave's LDS operations complete in order). The blocks it reads are this wave's own
+  // stores: they are waited for first.
+  if (nbw) {                                                  // wave-uniform
+    if (lane == 0) atomicAdd(S.nbail, nbw);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    tick_wave<N, false, false, true, true>(S, t0, nt, reinterpret_cast<uint32_t*>(img), (int)lane,
+                                           0, 1, blc, nbw, blt, blockIdx.x * 4 + wave);
+  }
+#ifdef RS_WAVELOG   // the wave's end: its stores issued, counted, its catch-up run
+  if (lane == 0 && S.wavelog) {
     const uint64_t wl_done = wall_clock64();
-    uint32_t* rec = S.wavelog + (size_t)(blockIdx.x * 4) * 32;
+    uint32_t* rec = S.wavelog + (size_t)(blockIdx.x * 4 + wave) * 32;
     rec[17] = (uint32_t)wl_done;
     rec[18] = (uint32_t)(wl_done >> 32);
   }
 #endif
-  if (nb == 0 || threadIdx.x >= 64) return;                   // wave-uniform
-  if (threadIdx.x == 0) atomicAdd(S.nbail, nb);
-  tick_wave<N, false, false, true, true>(S, t0, nt, dsm, (int)lane, 0, 1, bl_c, nb, bl_t,
-                                         blockIdx.x);
 }
 
 hipError_t configure_steady() {
