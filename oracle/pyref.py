@@ -95,10 +95,14 @@ def fnv(h, words):
     return h
 
 
-def fnv64(h, words):
-    """The trace hash's step (SIM_SPEC §4): the same multiply over 64-bit words."""
+# The trace hash's step (SIM_SPEC §4): a polynomial hash over 64-bit words, h <- h * M + x mod 2^64
+# (M odd: each step is a bijection of h)
+TRACE_M = 0x9E3779B97F4A7C15
+
+
+def trace_step(h, words):
     for w in words:
-        h = ((h ^ (w & M64)) * FNV_PRIME) & M64
+        h = (h * TRACE_M + (w & M64)) & M64
     return h
 
 
@@ -731,7 +735,7 @@ class PyCluster:
             except Halt as h:
                 self.fault[i] = h.code
                 self.cnt[["", "halt_ioobe", "halt_npe", "halt_cce", "halt_overflow"][h.code]] += 1
-                self.trace[i] = fnv64(self.trace[i], self._trace_words(t, ev, msg, node, h.code))
+                self.trace[i] = trace_step(self.trace[i], self._trace_words(t, ev, msg, node, h.code))
                 continue
             self.nodes[i] = new
             self.cnt[COUNTERS[ev - 1]] += 1
@@ -754,7 +758,7 @@ class PyCluster:
                     self.deadline[i] = t + cfg["hb"]
             elif ev == 6 or stats["rearm"] or node["state"] == ":leader":
                 self.deadline[i] = election
-            self.trace[i] = fnv64(self.trace[i], self._trace_words(t, ev, msg, new, 0))
+            self.trace[i] = trace_step(self.trace[i], self._trace_words(t, ev, msg, new, 0))
             for p, m in sends:
                 self.transmit(i, p, t, m, outbox, sides)
         # P2 delivery: receiver order, then sender id ascending, copy 0 then copy 1

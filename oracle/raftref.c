@@ -75,6 +75,8 @@ static uint32_t on_tick(uint64_t j, uint32_t P, uint32_t B) {
 #define FNV_OFFSET 0xCBF29CE484222325ull
 #define FNV_PRIME 0x100000001B3ull
 static uint64_t fnv(uint64_t h, uint32_t w) { return (h ^ w) * FNV_PRIME; }
+/* the trace hash's multiplier (SIM_SPEC §4): odd, so each step is a bijection of h */
+#define TRACE_M 0x9E3779B97F4A7C15ull
 
 /* ---------------------------------------------------------------- simulator state */
 struct shard {
@@ -391,10 +393,11 @@ static void redirect(tick_ctx_t* x, uint32_t k, const raft_msg_t* m, const uint3
 
 static uint64_t trace(uint64_t h, uint32_t t, uint32_t ev, uint32_t src, uint32_t mterm,
                       const raft_node_t* n, uint32_t fault) {
-  /* SIM_SPEC §4: two 64-bit words, (t | small << 32) then (msg_term | current_term << 32) */
+  /* SIM_SPEC §4: h <- h * M + x mod 2^64 over two 64-bit words, (t | small << 32) then
+     (msg_term | current_term << 32) */
   const uint64_t small = ev | src << 3 | n->role << 7 | fault << 9;
-  h = (h ^ ((uint64_t)t | small << 32)) * FNV_PRIME;
-  return (h ^ ((uint64_t)mterm | (uint64_t)n->current_term << 32)) * FNV_PRIME;
+  h = h * TRACE_M + ((uint64_t)t | small << 32);
+  return h * TRACE_M + ((uint64_t)mterm | (uint64_t)n->current_term << 32);
 }
 
 static uint32_t popcount16(uint32_t v) { return (uint32_t)__builtin_popcount(v & 0xFFFF); }

@@ -146,8 +146,8 @@ __host__ __device__ inline uint32_t sched_slots_bound(uint32_t C, uint32_t N) {
 }
 
 // Philox4x32-10 (Random123; round and key schedule of rocrand_philox4x32_10.h).
-__device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                        uint32_t k0, uint32_t k1) {
+__host__ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                 uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // one 32x32->64 product (v_mad_u64_u32) gives both halves (against a mul_lo + mul_hi pair:
@@ -237,20 +237,48 @@ __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;
 }
 
-// The trace hash's step (SIM_SPEC §4): FNV's multiply over two 64-bit words per event,
-// (t | (ev | src << 3 | role << 7 | fault << 9) << 32) then (msg_term | current_term << 32).
-// P = 2^40 + 0x1B3, so h * P = h * 0x1B3 + (h << 40): two products per word, both off the
-// other word's chain until the multiply.
-__device__ __forceinline__ uint64_t fnv64(uint64_t h, uint32_t lo, uint32_t hi) {
-  const uint32_t xl = (uint32_t)h ^ lo, xh = (uint32_t)(h >> 32) ^ hi;
-  // x * 0x1B3 + (x << 40): one v_mad_u64_u32 with the high word's products as its addend
-  return (uint64_t)xl * 0x1B3u + ((uint64_t)(xh * 0x1B3u + (xl << 8)) << 32);
+// The trace hash's step (SIM_SPEC §4): h <- (h * M + x0) * M + x1 mod 2^64 over two 64-bit words,
+// x0 = t | (ev | src << 3 | role << 7 | fault << 9) << 32, x1 = msg_term | current_term << 32,
+// computed as h * M^2 + (x0 * M + x1): the event's own term is off the hash's dependency chain,
+// which is one 64-bit multiply-add per event. A polynomial hash, so a run of events whose words
+// only shift by a constant tick offset folds into one multiply-add per run (steady_kernel.hip).
+constexpr uint64_t TRACE_M = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t TRACE_M2 = TRACE_M * TRACE_M;
+__device__ __forceinline__ uint64_t trace_term(uint32_t t, uint32_t ev, uint32_t src,
+                                               uint32_t mterm, uint32_t role, uint32_t term,
+                                               uint32_t fault) {
+  const uint64_t x0 = (uint64_t)t | (uint64_t)(ev | src << 3 | role << 7 | fault << 9) << 32;
+  const uint64_t x1 = (uint64_t)mterm | (uint64_t)term << 32;
+  return x0 * TRACE_M + x1;
 }
 __device__ __forceinline__ uint64_t trace_event(uint64_t h, uint32_t t, uint32_t ev, uint32_t src,
                                                 uint32_t mterm, uint32_t role, uint32_t term,
                                                 uint32_t fault) {
-  h = fnv64(h, t, ev | src << 3 | role << 7 | fault << 9);
-  return fnv64(h, mterm, term);
+  return h * TRACE_M2 + trace_term(t, ev, src, mterm, role, term, fault);
+}
+
+// A deferred timer in the stored state. A non-leader's re-armed deadline is t + el_base + the
+// EVENT draw of (its cluster, its id, t) scaled to el_span (SIM_SPEC D4); the kernels only compare
+// it with ticks at or past t + el_base, so they keep t + el_base and draw when a tick reaches it
+// (tick_wave's dpend, the steady kernel's fpend). FL_DRAW in the flags word carries that state
+// across launches: the stored deadline is the lower bound t + el_base and the draw is still owed.
+// Whatever reads the state resolves it (exact_deadline): the digest kernel, raft_sim_read_nodes;
+// the value is the one the draw would have given at any time.
+constexpr uint32_t FL_DRAW = 1u << 15;
+// The steady certificate: cluster word CL_CERT = CERT_MAGIC | L, written by the steady kernel for a
+// cluster it leaves at its fixed point (steady_kernel.hip) with node L as leader, promises that the
+// block's lines past the second hold that fixed point's words (empty logs, commit 0, the leader's
+// next / match rows 0) -- the next steady launch then reads the first two lines only. Every other
+// writer of a block clears it: the general tick body's write-back, raft_sim_write_nodes,
+// raft_sim_write_queue and raft_sim_write_clusters (whose reserved words it is; reads return them
+// zeroed), and the init kernel.
+constexpr uint32_t CL_CERT = 7;
+constexpr uint32_t CERT_MAGIC = 0x5EAD0000u;
+__host__ __device__ __forceinline__ uint32_t exact_deadline(uint32_t g, uint32_t id, uint32_t lb,
+                                                            uint32_t el_base, uint32_t el_span,
+                                                            uint32_t k0, uint32_t k1) {
+  const uint4 w = philox(g, id | P_EVENT << 8, lb - el_base, 0, k0, k1);
+  return lb + (uint32_t)(((uint64_t)w.y * el_span) >> 32);
 }
 
 // The EVENT draw of node id at tick t (SIM_SPEC §3): alts!! bit, timeout, rand-nth peer.

@@ -473,6 +473,10 @@ static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
     r.votes = mk & 0xFFFF; r.ls_keys = mk >> 16;
     r.current_term = f(rs::HF_TERM); r.commit_index = f(rs::HF_COMMIT);
     r.log_len = f(rs::HF_LEN); r.deadline = f(rs::HF_DEADLINE);
+    if (fl & rs::FL_DRAW)        // a deferred timer draw still owed in the stored state
+      r.deadline = rs::exact_deadline((uint32_t)(s->cfg.cluster_offset + c0 + i / N),
+                                      (uint32_t)(i % N) + 1, r.deadline, s->cfg.el_base,
+                                      s->cfg.el_span, s->d.key0, s->d.key1);
     for (size_t p = 0; p < N; ++p) {
       r.next_index[p] = (int32_t)f(rs::HF_NEXT + p);
       r.match_index[p] = (int32_t)f(rs::HF_NEXT + N + p);
@@ -528,6 +532,7 @@ static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t*
       f(rs::HF_NEXT + N + p) = (uint32_t)r.match_index[p];
     }
   }
+  for (size_t c = 0; c < nc; ++c) blk[c * HB + rs::CL_CERT] = 0;   // the steady certificate
   HIP_OK(h2d(s, s->d.hot + (size_t)c0 * HB, blk.data(), nc * HB));
   HIP_OK(h2d(s, s->d.ccount + n0, ccv.data(), cnt));
   HIP_OK(hipStreamSynchronize(s->stream));
@@ -586,6 +591,8 @@ static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t whic
   HIP_OK(h2d(s, hot_word(s, cluster, id, rs::HF_QMETA), &qm, 1));
   HIP_OK(h2d(s, hot_word(s, cluster, id, which ? rs::HF_RES_ARR : rs::HF_REQ_ARR), &harr, 1));
   HIP_OK(h2d(s, hot_word(s, cluster, id, which ? rs::HF_RES_TAIL : rs::HF_REQ_TAIL), &tail, 1));
+  const uint32_t zero = 0;                                        // the steady certificate
+  HIP_OK(h2d(s, cl_words(s, cluster) + rs::CL_CERT, &zero, 1));
   HIP_OK(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -713,6 +720,8 @@ static int sh_read_clusters(Shard* s, uint32_t c0, uint32_t nc, raft_cluster_t* 
     HIP_OK(hipMemcpy2DAsync(out, sizeof(raft_cluster_t), cl_words(s, c0), (size_t)s->d.HB * 4,
                             sizeof(raft_cluster_t), nc, hipMemcpyDeviceToHost, s->stream));
   HIP_OK(hipStreamSynchronize(s->stream));
+  // the reserved words are the kernels' (the steady certificate, rs::CL_CERT): not state
+  for (uint32_t i = 0; i < nc; ++i) out[i].reserved[0] = out[i].reserved[1] = out[i].reserved[2] = 0;
   return 0;
 }
 

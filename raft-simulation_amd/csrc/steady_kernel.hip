@@ -52,15 +52,17 @@ __device__ __forceinline__ uint32_t msel(bool a, uint32_t x, uint32_t y) {
 // four 128-B lines at N >= 4) in LDS: loads and stores then move whole lines, eight lines per wave
 // instruction, where a lane reading its own cluster's block straight into registers touches 64
 // lines per instruction (one per lane, the texture path's rate) -- the load phase's cost.
-// Chunk i of the wave's cluster l sits in slot i ^ (l & 15) of l's 512-B row: the LDS-DMA loads
-// (global_load_lds: lane-linear destination) take the swizzle on their source addresses, and a
-// lane reading chunk i of its own cluster, or writing it back, meets no bank conflict (the 16 lanes
-// of a ds_read_b128 group have distinct l & 15).
-constexpr int IMG_SLOTS = 32;                               // slots per cluster row
-constexpr uint32_t IMG_ROW = IMG_SLOTS * 16;                // bytes
-constexpr uint32_t IMG_WAVE = 64 * IMG_ROW;                 // 32 KiB per wave
+// Two halves: lines 0-1 of every cluster, then lines 2-3 (loaded only when some cluster of the
+// wave has no steady certificate, device.hpp). In a half, chunk i of the wave's cluster l sits in
+// slot i ^ (l & 15) of l's 256-B row: the LDS-DMA loads (global_load_lds: lane-linear destination)
+// take the swizzle on their source addresses, and a lane reading chunk i of its own cluster, or
+// writing it back, meets no bank conflict (the 16 lanes of a ds_read_b128 group have distinct
+// l & 15).
+constexpr int IMG_SLOTS = 32;                               // chunks per cluster, both halves
+constexpr uint32_t IMG_HALF = 64 * 16 * 16;                 // 16 KiB: 64 clusters x 16 chunks
+constexpr uint32_t IMG_WAVE = 2 * IMG_HALF;                 // 32 KiB per wave
 __device__ __forceinline__ uint32_t img_off(uint32_t l, uint32_t i) {
-  return l * IMG_ROW + 16u * (i ^ (l & 15u));
+  return (i >> 4) * IMG_HALF + l * 256u + 16u * ((i & 15u) ^ (l & 15u));
 }
 template <typename T>
 __device__ __forceinline__ T* lds_at(char* img, uint32_t off) {
@@ -74,6 +76,23 @@ template <int N>
 constexpr size_t steady_lds_bytes() {
   static_assert(block_lds_bytes<N, false>() <= IMG_WAVE, "the catch-up block fits a wave's image");
   return 4 * (size_t)IMG_WAVE;
+}
+
+// M2^n and 1 + M2 + ... + M2^(n-1) mod 2^64 (the trace hash's multiplier per event, device.hpp)
+template <int n>
+__host__ __device__ constexpr uint64_t trace_pow() {
+  uint64_t x = 1;
+  for (int i = 0; i < n; ++i) x *= TRACE_M2;
+  return x;
+}
+template <int n>
+__host__ __device__ constexpr uint64_t trace_geo() {
+  uint64_t s = 0, x = 1;
+  for (int i = 0; i < n; ++i) {
+    s += x;
+    x *= TRACE_M2;
+  }
+  return s;
 }
 
 // Wave-wide sum (all 64 lanes active), uniform: DPP row shifts and broadcasts as in wave_min.
@@ -147,26 +166,52 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #endif
 
   // ------------------------------------------- load: the wave's blocks into its image (LDS-DMA)
-  {
-    const uint32_t p = lane & 31;
+  // half h (lines 2h, 2h + 1): wave instruction j takes clusters 4j .. 4j + 3, 16 slots each
+  auto load_half = [&](int h) {
+    const uint32_t p = lane & 15;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {                  // clusters 2j, 2j + 1: 32 slots each
-      const uint32_t cc = 2 * j + (lane >> 5);
-      const uint32_t i = p ^ (cc & 15u);
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t cc = 4 * j + (lane >> 4);
+      const uint32_t i = 16 * h + (p ^ (cc & 15u));
       const uint32_t cg = min(cbase + cc, S.C - 1);  // past the shard's end: any block, unused
       if (i < (uint32_t)IMGC)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(S.hot + (size_t)cg * HB + 4 * i),
-            (__attribute__((address_space(3))) void*)(img + j * 1024), 16, 0, 0);
+            (__attribute__((address_space(3))) void*)(img + h * IMG_HALF + j * 1024), 16, 0, 0);
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's own LDS-DMA writes have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's own LDS-DMA writes landed
+  };
   uint32_t w[NW4 * 4];
 #pragma unroll
-  for (int i = 0; i < NW4; ++i) {
+  for (int i = 0; i < NW4 * 4; ++i) w[i] = 0;
+  load_half(0);
+#pragma unroll
+  for (int i = 0; i < (NW4 < 16 ? NW4 : 16); ++i) {
     const uint4 x = *lds_at<const uint4>(img, img_off(lane, i));
     w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
   }
+  // The steady certificate (device.hpp): a cluster the last steady launch left at its fixed point
+  // with leader L needs only the first two lines. The rest is loaded when some cluster of the wave
+  // lacks one; otherwise those words read as the fixed point's (zero).
+  uint32_t Lc = 0, nlc = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const bool lead = (w[HOT_CW + HF_FLAGS * N + k] & 3) == RAFT_LEADER;
+    Lc = lead ? (uint32_t)k : Lc;
+    nlc += lead;
+  }
+  static_assert(HOT_CW + (HF_FLAGS + 1) * N <= 64, "the flags are in the first two lines");
+  const bool cert = active && nlc == 1 && w[CL_CERT] == (CERT_MAGIC | Lc);
+  const bool full = IMGC > 16 && __builtin_amdgcn_ballot_w64(active && !cert) != 0;   // uniform
+  if (full) {
+    load_half(1);
+#pragma unroll
+    for (int i = 16; i < NW4; ++i) {
+      const uint4 x = *lds_at<const uint4>(img, img_off(lane, i));
+      w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+    }
+  }
+  const bool vouched = cert && !full;         // its lines past the second are the fixed point's
 #ifdef RS_WAVELOG
   wl_loop = wall_clock64();
 #endif
@@ -185,7 +230,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     const bool lead = (f & 3) == RAFT_LEADER;
     L = lead ? (uint32_t)k : L;
     nlead += lead;
-    badn |= ((f >> 10) & 7) | (lead != (((f >> 14) & 1) != 0));
+    badn |= ((f >> 10) & 7) | (lead != (((f >> 14) & 1) != 0)) | (lead && (f & FL_DRAW));
   }
   bool bad = !active || nlead != 1 || badn != 0 || S.Q < (uint32_t)F;
   const uint32_t Lid = L + 1;
@@ -337,14 +382,17 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     if (!rmask) resA = INF;
   }
   record_bail(active && bad, t0);           // outside the model from the start: bail at t0
-  const bool wb = active && !bad;
+  bool wb = active && !bad;
   bool run = wb;
 
   // ---------------------------------------------------------------- the cluster's ticks
   const uint32_t tend = t0 + nt, d = S.dmin;
   uint32_t tn = t0, nhb = 0, nae = 0, nar = 0;
   // followers whose deadline holds its lower bound t_ae + el_base (the draw is deferred)
+  // (a draw owed from an earlier launch: FL_DRAW in the follower's flags, device.hpp)
   uint32_t fpend = 0;
+#pragma unroll
+  for (int j = 0; j < F; ++j) fpend |= ((ffl[j] & FL_DRAW) ? 1u : 0u) << j;
   auto draw_deadlines = [&](uint32_t due) {
 #pragma unroll
     for (int j = 0; j < F; ++j) {
@@ -361,6 +409,184 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     for (int j = 0; j < F; ++j) m = min(m, min(fdl[j], qA[j]));
     return m;
   };
+  const uint32_t P = 2 * d + F - 1 + S.hb, last = 2 * d + F - 1, allF = (1u << F) - 1;
+  // The cluster at its fixed point: every follower took the leader's append-entries (flags,
+  // votes, term and commit are what another one sets again), every response succeeded (next /
+  // match / keys as another one sets them), the log is empty (a heartbeat ships nothing) and no
+  // message is in flight. If the followers' re-armed timers (>= t_ae + el_base) cannot fire
+  // before the next round's append-entries (el_base >= the round period P) and the leader's
+  // responses all fit before its next heartbeat (hb >= 2d + F), every later round is this one
+  // shifted by a multiple of P: only the ticks in the trace hashes change.
+  auto at_fixed_point_state = [&]() {
+    bool ok = Llen == 0 && !ackbad;
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+      ok = ok && fterm[j] == Lterm &&
+           (ffl[j] & (3u | 15u << 2 | 15u << 6 | 1u << 13)) == (RAFT_FOLLWER | Lid << 6) &&
+           fcommit[j] == flen[j] && (fmk[j] & 0xFFFFu) == 0 && nx[j] == 0 &&
+           mt[j] == (int32_t)Lcommit;
+    return ok;
+  };
+  auto at_fixed_point = [&]() {
+    return S.el_base >= P && S.hb >= 2 * d + F && !qmask && !rmask && at_fixed_point_state();
+  };
+  // From the fixed point with the next heartbeat at th, every round to the launch's end as trace
+  // hashes: the rounds that end before it, then the one it cuts (heartbeat, append-entries and
+  // responses up to tend - 1; what is left is queued as the general body leaves it): every next
+  // event of the cluster is then at or after tend.
+  auto fixed_point_rounds = [&](uint32_t th) {
+    const uint32_t K = tend > th + last ? (tend - th - last - 1) / P + 1 : 0;
+    uint32_t tk = th + K * P;
+    if (K) {
+      // The trace hash is polynomial (device.hpp): a round's F + 1 leader events take the
+      // leader's hash h to h * M2^(F+1) + a, with a the Horner sum of the events' terms, and a
+      // round P ticks later adds P * M * (1 + M2 + ... + M2^F) to a; a follower's one event per
+      // round takes h to h * M2 + c, and c grows by P * M. One multiply-add per hash per round.
+      uint64_t a = trace_term(th, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        a = a * TRACE_M2 + trace_term(th + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
+                                      RAFT_LEADER, Lterm, 0);
+      const uint64_t da = (uint64_t)P * (TRACE_M * trace_geo<F + 1>());
+      const uint64_t df = (uint64_t)P * TRACE_M;
+      uint64_t cf[F];
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        cf[j] = trace_term(th + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER, Lterm, 0);
+      for (uint32_t r = 0; r < K; ++r) {
+        Ltr = Ltr * trace_pow<F + 1>() + a;
+        a += da;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          ftr[j] = ftr[j] * TRACE_M2 + cf[j];
+          cf[j] += df;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < F; ++j) fdl[j] = tk - P + d + S.el_base;   // + the deferred draw
+      fpend = (1u << F) - 1;
+      Ldl = tk;                                   // = the last response + hb
+      nhb += K;
+      nae += F * K;
+      nar += F * K;
+    }
+    if (tk < tend) {                              // the round the launch's end cuts
+      Ltr = trace_event(Ltr, tk, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+      ++nhb;
+      Ldl = tk + S.hb;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        qA[j] = tk + d; qT[j] = Lterm; qa[j] = Lcommit; qb[j] = 0;
+      }
+      qmask = (1u << F) - 1;
+      if (tk + d < tend) {                        // the append-entries, then responses in time
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          ftr[j] = trace_event(ftr[j], tk + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
+                               Lterm, 0);
+          fdl[j] = tk + d + S.el_base;
+          rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
+          qA[j] = INF;
+        }
+        fpend = (1u << F) - 1;
+        qmask = 0;
+        rmask = (1u << F) - 1;
+        resA = tk + 2 * d;
+        nae += F;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          if (tk + 2 * d + j < tend) {
+            Ltr = trace_event(Ltr, tk + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
+                              RAFT_LEADER, Lterm, 0);
+            rmask &= ~(1u << j);
+            Ldl = tk + 2 * d + j + S.hb;
+            ++nar;
+          }
+        }
+      }
+    }
+  };
+
+  // ------------------------------------------- the fixed-point path (C2's steady state)
+  // A cluster at its fixed point (above) whose round in progress at t0 is on the period-P
+  // schedule -- none (the next heartbeat at Ldl >= t0), its append-entries in flight, or its
+  // responses pending exactly as the last launch's end cut them -- and whose followers' timers
+  // cannot fire before their next append-entries runs every event of the launch here: the rest
+  // of that round event by event, then fixed_point_rounds. Everything else is the general loop's.
+  bool fp = wb && S.el_base >= P && S.hb >= 2 * d + F && (vouched || at_fixed_point_state());
+  uint32_t th0 = Ldl, mid = 0;               // the round's heartbeat; 1 AEs in flight, 2 responses
+  if (qmask) {
+    mid = 1;
+    th0 = qA[0] - d;
+    fp = fp && qmask == allF && !rmask && qA[0] >= t0 && qA[0] >= d && Ldl == th0 + S.hb;
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+      fp = fp && qA[j] == qA[0] && qT[j] == Lterm && qa[j] == Lcommit && qb[j] == 0;
+  } else if (rmask) {
+    mid = 2;
+    th0 = resA - 2 * d;
+    const uint32_t j0 = (uint32_t)F - __popc(rmask);          // responses already taken
+    const int64_t cut = (int64_t)t0 - ((int64_t)th0 + 2 * d);  // what the last launch's end cut
+    fp = fp && resA >= 2 * d && rmask == (allF & ~((1u << j0) - 1)) &&
+         (int64_t)j0 == (cut < 0 ? 0 : cut > F ? (int64_t)F : cut) &&
+         Ldl == (j0 ? th0 + 2 * d + j0 - 1 : th0) + S.hb;
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+      fp = fp && (!((rmask >> j) & 1) ||
+                  (rT[j] == Lterm && rA[j] == Lcommit && rB[j] == 0 && rH[j] == 1));
+  } else {
+    fp = fp && Ldl >= t0;
+  }
+  {
+    const uint32_t nxt = min((mid == 2 ? th0 + P : th0) + d, tend);   // the next AE (or the end)
+#pragma unroll
+    for (int j = 0; j < F; ++j) fp = fp && fdl[j] >= nxt;
+  }
+  // A vouched cluster off the fixed-point path (set_tick moved the clock, ...) has no full state
+  // here: the general body runs it from t0.
+  const bool vbail = vouched && wb && !fp;
+  record_bail(vbail, t0);
+  if (vbail) wb = run = false;
+  if (fp) {
+    run = false;
+    bool whole = true;                        // the round in progress finished in this launch
+    if (mid == 1) {
+      const uint32_t ta = qA[0];
+      if (ta < tend) {                        // the append-entries
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
+                               Lterm, 0);
+          fdl[j] = ta + S.el_base;
+          qA[j] = INF;
+          rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
+        }
+        fpend = allF;
+        qmask = 0;
+        rmask = allF;
+        resA = ta + d;
+        nae += F;
+      } else {
+        whole = false;
+      }
+    }
+    if (mid && whole) {                       // the responses, one per tick in slot order
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const uint32_t tau = th0 + 2 * d + j;
+        if (((rmask >> j) & 1) && tau < tend) {
+          Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm, RAFT_LEADER,
+                            Lterm, 0);
+          rmask &= ~(1u << j);
+          Ldl = tau + S.hb;
+          ++nar;
+        }
+      }
+      if (rmask) whole = false;
+      else resA = INF;
+    }
+    if (whole) fixed_point_rounds(mid ? th0 + P : th0);
+  }
 #ifdef RS_WAVELOG
   wl_ts = __builtin_amdgcn_s_memtime();
 #endif
@@ -521,37 +747,9 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         go = go && t + 2 * d + j < tend &&
              response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
       if (!rmask) resA = INF;
-      // A round that ran every response leaves the cluster in its fixed point: every follower
-      // took the append-entries (its flags, votes, term and commit are what another one sets
-      // again) and every response succeeded (next / match / keys as another one sets them). If
-      // the followers' re-armed timers (>= t_ae + el_base) cannot fire before the next round's
-      // append-entries (el_base >= the round period P), the next heartbeat (last response + hb) is
-      // the cluster's next event, and every later round that ends before the launch does is
-      // this one shifted by a multiple of P: only the ticks in the trace hashes change. Those
-      // rounds run here as hashes alone, with the state and counters of the last one.
-      const uint32_t P = 2 * d + F - 1 + S.hb;
-      if (!rmask && S.el_base >= P && tend - t > P + 2 * d + F) {
-        const uint32_t R = (tend - t - 2 * d - F - 1) / P;       // more rounds that end in time
-        uint32_t tk = t;
-        for (uint32_t r = 0; r < R; ++r) {
-          tk += P;
-          Ltr = trace_event(Ltr, tk, 7, 0, 0, RAFT_LEADER, Lterm, 0);
-#pragma unroll
-          for (int j = 0; j < F; ++j)
-            ftr[j] = trace_event(ftr[j], tk + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
-                                 Lterm, 0);
-#pragma unroll
-          for (int j = 0; j < F; ++j)
-            Ltr = trace_event(Ltr, tk + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
-                              RAFT_LEADER, Lterm, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < F; ++j) fdl[j] = tk + d + S.el_base;   // deferred draws (fpend)
-        Ldl = tk + 2 * d + F - 1 + S.hb;
-        tl = tk + 2 * d + F - 1;
-        nhb += R;
-        nae += F * R;
-        nar += F * R;
+      if (at_fixed_point()) {
+        fixed_point_rounds(t + P);
+        tl = tend - 1;                       // nothing of the cluster is left before tend
       }
     } else if (fae || lres) {
       // fae: the append-entries at t, then their responses from t + d in the same trip unless
@@ -559,7 +757,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       // sender order, while nothing else in the cluster is due (the followers' next events and
       // the launch end; the leader's own deadline moves past each); lres: the first one at t
       // was decided above. A response outside the model ends the run and the next trip
-      // decides it.
+      // decides it. A round finished here (one the last launch cut) continues at the fixed point.
       uint32_t tau0 = t;
       if (fae) {
         append_entries(t, fae);
@@ -578,11 +776,16 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         if (!ok) break;
         if (!rmask) resA = INF;
       }
+      if (at_fixed_point() && Ldl > tl) {
+        fixed_point_rounds(Ldl);
+        tl = tend - 1;
+      }
     }
     RS_LPH(4);
     tn = tl + 1;
   }
-  draw_deadlines(fpend);                     // every deadline exact before it is stored
+  // the draws still owed stay owed in the stored state (FL_DRAW): a cluster at its fixed point
+  // makes none at all
 
 #ifdef RS_WAVELOG
   const uint64_t wl_lend = wall_clock64();
@@ -604,6 +807,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
   }
   uint32_t dl = 0;                           // lines of the cluster's block changed
+  const bool wfp = !__builtin_amdgcn_ballot_w64(wb && !fp);
   if (wb) {
     // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
     constexpr int NV = HF_NEXT;
@@ -620,7 +824,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       const uint64_t trf = (uint64_t)msel(lo, (uint32_t)(ftr[jl] >> 32), (uint32_t)(ftr[jh] >> 32)) << 32 |
                           msel(lo, (uint32_t)ftr[jl], (uint32_t)ftr[jh]);
       const uint64_t tr = isL ? Ltr : trf;
-      v[HF_FLAGS][k] = isL ? Lfl : fv(ffl);
+      v[HF_FLAGS][k] = isL ? Lfl : (fv(ffl) & ~FL_DRAW) | (((fpend >> (lo ? jl : jh)) & 1) ? FL_DRAW : 0u);
       v[HF_MASKS][k] = isL ? Lmk : fv(fmk);
       v[HF_TERM][k] = isL ? Lterm : fv(fterm);
       v[HF_COMMIT][k] = isL ? Lcommit : fv(fcommit);
@@ -639,35 +843,50 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     // The changed chunks into the image (in a heartbeat round the deadlines and trace hashes
     // change, all in the block's first line; flags, terms, masks, commits, queue words and rows
     // come back unchanged); the lines they dirty go back to memory whole, below.
+    // A wave whose written-back clusters all took the fixed-point path changed nothing past the
+    // queue words and the flags' FL_DRAW (masks, terms, commits, lengths and rows are the fixed
+    // point's).
+    const int ch_end = wfp ? (int)(HOT_CW + (HF_FLAGS + 1) * N + 3) / 4
+                           : (int)(HOT_CW + HF_NEXT * N + 3) / 4;
+    // (every chunk is written back to the image, changed or not: no branch per chunk)
 #pragma unroll
     for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_NEXT * N + 3) / 4; ++i) {
-      const int q = 4 * i;
-      const uint4 x = make_uint4(live(q) ? val(q) : w[q], live(q + 1) ? val(q + 1) : w[q + 1],
-                                 live(q + 2) ? val(q + 2) : w[q + 2],
-                                 live(q + 3) ? val(q + 3) : w[q + 3]);
-      if (x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3]) {
+      if (i < ch_end) {                                    // wave-uniform
+        const int q = 4 * i;
+        const uint4 x = make_uint4(live(q) ? val(q) : w[q], live(q + 1) ? val(q + 1) : w[q + 1],
+                                   live(q + 2) ? val(q + 2) : w[q + 2],
+                                   live(q + 3) ? val(q + 3) : w[q + 3]);
         *lds_at<uint4>(img, img_off(lane, i)) = x;
-        dl |= 1u << (i / 8);
+        dl |= (uint32_t)(x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3])
+              << (i / 8);
       }
     }
+    // the steady certificate for the next launch: the cluster stays at its fixed point
+    const uint32_t cn = fp || (full && at_fixed_point_state()) ? (CERT_MAGIC | L) : 0u;
+    *lds_at<uint4>(img, img_off(lane, CL_CERT / 4)) = make_uint4(w[4], w[5], w[6], cn);
+    dl |= (uint32_t)(cn != w[CL_CERT]);
     // the leader's rows (node L): next / match of peer fk(j) + 1
+    if (!wfp) {
 #pragma unroll
-    for (int j = 0; j < F; ++j) {
-      const uint32_t qn = HOT_CW + (HF_NEXT + fk(j)) * N + L;
-      const uint32_t qt = HOT_CW + (HF_NEXT + N + fk(j)) * N + L;
-      if (nx[j] != nx0[j]) {
-        *lds_at<uint32_t>(img, img_off(lane, qn / 4) + 4 * (qn % 4)) = (uint32_t)nx[j];
-        dl |= 1u << (qn / 32);
-      }
-      if (mt[j] != mt0[j]) {
-        *lds_at<uint32_t>(img, img_off(lane, qt / 4) + 4 * (qt % 4)) = (uint32_t)mt[j];
-        dl |= 1u << (qt / 32);
+      for (int j = 0; j < F; ++j) {
+        const uint32_t qn = HOT_CW + (HF_NEXT + fk(j)) * N + L;
+        const uint32_t qt = HOT_CW + (HF_NEXT + N + fk(j)) * N + L;
+        if (nx[j] != nx0[j]) {
+          *lds_at<uint32_t>(img, img_off(lane, qn / 4) + 4 * (qn % 4)) = (uint32_t)nx[j];
+          dl |= 1u << (qn / 32);
+        }
+        if (mt[j] != mt0[j]) {
+          *lds_at<uint32_t>(img, img_off(lane, qt / 4) + 4 * (qt % 4)) = (uint32_t)mt[j];
+          dl |= 1u << (qt / 32);
+        }
       }
     }
-    // queues back to the rings, heads at slot 0 (a message in flight at the launch's end: rare)
+  }
+  // queues back to the rings, heads at slot 0 (a message in flight at the launch's end: rare)
+  if (__builtin_amdgcn_ballot_w64(wb && (qmask || rmask))) {            // wave-uniform
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      if ((qmask >> j) & 1) {
+      if (wb && ((qmask >> j) & 1)) {
         uint4* dp = reinterpret_cast<uint4*>(qslots(S, c * N + fk(j), 0));
         dp[0] = make_uint4(qA[j], RAFT_MSG_APPEND_ENTRIES | Lid << 3, qT[j], qa[j]);
         dp[1] = make_uint4(qb[j], 0, 0, 0);
@@ -677,7 +896,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     uint32_t n = 0;
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      if ((rmask >> j) & 1) {
+      if (wb && ((rmask >> j) & 1)) {
         const uint32_t sid = fk(j) + 1;
         uint4* dp = rp + 2 * n;
         dp[0] = make_uint4(resA, RAFT_MSG_APPEND_RESPONSE | sid << 3 | rH[j] << 7, rT[j], rA[j]);
@@ -687,17 +906,31 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
   }
   // Dirty lines back to memory whole: a wave instruction writes eight clusters' line (8 lanes x
-  // 16 B each), read from the image (line ln of cluster cc is its chunks 8 ln .. 8 ln + 7).
+  // 16 B each), read from the image (line ln of cluster cc is its chunks 8 ln .. 8 ln + 7): the
+  // eight reads of a line first, then the stores. The stores write through to memory (sc1: the
+  // lines leave the XCD's L2 as the waves end, not at the launch's end; the next launch reads them
+  // from the Infinity Cache either way). They are not in the compiler's wait counts: the catch-up
+  // below waits for them itself.
+  {
+    uint32_t* const wbase = S.hot + (size_t)cbase * HB;      // the wave's first block
+    const uint32_t sub = lane >> 3, q8 = lane & 7;
 #pragma unroll
-  for (int ln = 0; ln < IMGC / 8; ++ln) {
-    const uint64_t bal = __builtin_amdgcn_ballot_w64((dl >> ln) & 1);
-    if (!bal) continue;                                  // wave-uniform
+    for (int ln = 0; ln < IMGC / 8; ++ln) {
+      const uint64_t bal = __builtin_amdgcn_ballot_w64((dl >> ln) & 1);
+      if (!bal) continue;                                  // wave-uniform
+      uint4 xs[8];
 #pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-      const uint32_t cc = 8 * gq + (lane >> 3), q = 8 * ln + (lane & 7);
-      if ((bal >> cc) & 1) {
-        const uint4 x = *lds_at<const uint4>(img, img_off(cc, q));
-        *reinterpret_cast<uint4*>(S.hot + (size_t)(cbase + cc) * HB + 4 * q) = x;
+      for (int gq = 0; gq < 8; ++gq)
+        xs[gq] = *lds_at<const uint4>(img, img_off(8 * gq + sub, 8 * ln + q8));
+#pragma unroll
+      for (int gq = 0; gq < 8; ++gq) {
+        const uint32_t cc = 8 * gq + sub;
+        if ((bal >> cc) & 1) {
+          typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+          const v4u xv = {xs[gq].x, xs[gq].y, xs[gq].z, xs[gq].w};
+          uint32_t* const dst = wbase + cc * HB + 4 * (8 * ln + q8);
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(xv) : "memory");
+        }
       }
     }
   }

@@ -245,10 +245,12 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
     const uint32_t gi = c * N + k;
     const uint32_t* hw = hot_node(S, c, k);
     const uint32_t fl = hw[HF_FLAGS * N], mk = hw[HF_MASKS * N], qm = hw[HF_QMETA * N];
+    const uint32_t dl = (fl & FL_DRAW) ? exact_deadline(S.goff + c, k + 1, hw[HF_DEADLINE * N],
+                                                        S.el_base, S.el_span, S.key0, S.key1)
+                                       : hw[HF_DEADLINE * N];
     const uint32_t w[12] = {fl & 3, (fl >> 2) & 15, (fl >> 6) & 15, (fl >> 10) & 7,
                             (fl >> 13) & 1, (fl >> 14) & 1, mk & 0xFFFF, mk >> 16,
-                            hw[HF_TERM * N], hw[HF_COMMIT * N], hw[HF_LEN * N],
-                            hw[HF_DEADLINE * N]};
+                            hw[HF_TERM * N], hw[HF_COMMIT * N], hw[HF_LEN * N], dl};
     for (int i = 0; i < 12; ++i) h = fnv(h, w[i]);
     for (uint32_t p = 0; p < 2 * N; ++p) h = fnv(h, hw[(HF_NEXT + p) * N]);   // next, then match
     h = fnv(h, hw[hf_led(N) * N]);

@@ -482,6 +482,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       n.votes = mk & 0xFFFF; n.keys = mk >> 16 | ((fl >> 14) & 1);
       n.term = hp[HF_TERM * N]; n.commit = hp[HF_COMMIT * N]; n.len = hp[HF_LEN * N];
       n.deadline = hp[HF_DEADLINE * N];
+      if (!SPEC) dpend[lane] = (fl & FL_DRAW) ? 1u : 0u;   // a deferred draw carried over
       n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
       n.rq.arr = hp[HF_REQ_ARR * N]; n.rs.arr = hp[HF_RES_ARR * N];
       n.rq.tail = hp[HF_REQ_TAIL * N]; n.rs.tail = hp[HF_RES_TAIL * N];
@@ -1505,11 +1506,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #endif
 
     // ---------------------------------------------------------------- write back
-    if (!SPEC && active && dpend[lane]) {       // every deadline exact before it is stored
-      const uint4 wd = event_draw(g, (uint32_t)k0 + 1, n.deadline - S.el_base, S);
-      n.deadline += __umulhi(wd.y, S.el_span);
-      dpend[lane] = 0;
-    }
+    // a deferred draw stays owed in the stored state (FL_DRAW, device.hpp)
+    const uint32_t owed = !SPEC && active && dpend[lane] ? FL_DRAW : 0u;
+    if (!SPEC) dpend[lane] = 0;
     if (S.shist) {
       // RAFT_SCHED_ALIGNED: the cluster's packing key relative to the next launch, counted into the
       // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
@@ -1547,7 +1546,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       asm volatile("" : "+v"(cw));
       uint32_t* const hp = S.hot + (size_t)cw * HB + HOT_CW + k0;
       uint32_t* const hc = S.hot + (size_t)cw * HB + CLW;
-      hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.keys & 1u);
+      hp[HF_FLAGS * N] = pack_flags(n.role, n.vf, n.lid, n.fault, n.seq, n.keys & 1u) | owed;
       hp[HF_MASKS * N] = n.votes | (n.keys & ~1u) << 16;
       hp[HF_TERM * N] = n.term; hp[HF_COMMIT * N] = n.commit; hp[HF_LEN * N] = n.len;
       hp[HF_DEADLINE * N] = n.deadline;
@@ -1565,6 +1564,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       }
       if (k0 == 0) {
         hc[0] = hidx; hc[1] = hterm; hc[2] = hval; hc[3] = cnext; hc[4] = ccount;
+        hc[CL_CERT] = 0;                    // the steady certificate no longer holds (device.hpp)
       }
     }
   } while (CATCH && (wave += wstride) * CPW < nslots);   // the general grid covers every slot

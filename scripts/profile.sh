@@ -8,8 +8,8 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_${TAG}_${WL}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-# the bench defaults (20 steps, 2 warm-up): the same window as the driver's bench line
-B="$R/bench.py --workload $WL --steps 20 --warmup 2 --no-cpu-baseline"
+# the bench defaults (20 steps, 5 warm-up): the same window as the driver's bench line
+B="$R/bench.py --workload $WL --steps 20 --warmup 5 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $B > $OUT/kt.log 2>&1 || { echo "kt failed $?"; exit 1; }
 echo "kt ok"
 i=0

@@ -1,8 +1,12 @@
+# Round-5 working session on the GPU box: the -m gpu suite (or a -k subset), the C2 dispatch A/B
+# against the libraries given, and the C2 lane timeline of the -DRS_WAVELOG build.
+# Usage: bash scripts/r5_session.sh "[pytest -k expression, empty for all]" [LIB ...]
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 L=raft-simulation_amd/build
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bench_windows.py -x -v --timeout 200 --timeout-method thread -k "steady or lite or c2 or host_writes" > gpurun_out/r5b_tests.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error" gpurun_out/r5b_tests.log | head; tail -30 gpurun_out/r5b_tests.log; exit 1; }
-tail -2 gpurun_out/r5b_tests.log
-timeout -k 10 120 python scripts/dispatch_probe.py $L/libraftsim_r4.so $L/libraftsim.so > gpurun_out/r5b_probe.txt 2>&1 || { echo "probe failed"; tail gpurun_out/r5b_probe.txt; exit 1; }
-cat gpurun_out/r5b_probe.txt
-timeout -k 10 120 python scripts/lane_timeline.py $L/libraftsim_wavelog.so > gpurun_out/r5b_timeline.txt 2>&1 || { echo "timeline failed"; tail gpurun_out/r5b_timeline.txt; exit 1; }
-cat gpurun_out/r5b_timeline.txt
+KEXPR=$1; shift
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${KEXPR:+-k "$KEXPR"} > gpurun_out/r5_tests.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error" gpurun_out/r5_tests.log | head; tail -30 gpurun_out/r5_tests.log; exit 1; }
+tail -2 gpurun_out/r5_tests.log
+timeout -k 10 120 python scripts/dispatch_probe.py "$@" $L/libraftsim.so > gpurun_out/r5_probe.txt 2>&1 || { echo "probe failed"; tail gpurun_out/r5_probe.txt; exit 1; }
+cat gpurun_out/r5_probe.txt
+timeout -k 10 120 python scripts/lane_timeline.py $L/libraftsim_wavelog.so > gpurun_out/r5_timeline.txt 2>&1 || { echo "timeline failed"; tail gpurun_out/r5_timeline.txt; exit 1; }
+cat gpurun_out/r5_timeline.txt

@@ -168,12 +168,16 @@ def _client_set_into(be, cluster, node, value):
 
 
 @pytest.mark.parametrize("mode", ["auto", "always"])
-@pytest.mark.parametrize("event", ["set_tick", "client_set", "client_cursor"])
+@pytest.mark.parametrize("event", ["set_tick", "client_set", "client_cursor", "node_term",
+                                   "node_log"])
 def test_gpu_host_writes_after_lite_launches(event, mode, monkeypatch):
     """Host writes after 14 LITE launches (past the 8-launch packing period, with the packing
     reused between rebuilds): set_tick, a queued client-set and a finite client cursor (both clear
-    LITE for the rest of the handle) land at every phase of the rebuild cycle; GPU == oracle after
-    each of the next 10 launches (raftsim.hip: packing keys and histogram stay consistent)."""
+    LITE for the rest of the handle), and node records rewritten under clusters the steady kernel
+    left with a certificate (a follower's term raised; a log entry given to a leader and committed:
+    raft_sim_write_nodes clears the certificate, device.hpp) land at every phase of the rebuild
+    cycle; GPU == oracle after each of the next 10 launches (raftsim.hip: packing keys and
+    histogram stay consistent)."""
     monkeypatch.setenv("RAFTSIM_STEADY", mode)
     cfg = dict(n_clusters=4096, nodes=5, seed=42, ticks_per_launch=1000, log_cap=64)
     for phase in (0, 3):
@@ -188,9 +192,22 @@ def test_gpu_host_writes_after_lite_launches(event, mode, monkeypatch):
             elif event == "client_set":
                 for c in (5, 100, 4095):
                     _client_set_into(be, c, 1 + c % 5, 1000 + c)
-            else:
+            elif event == "client_cursor":
                 be.write_clusters(7, [dict(hwm=(0, 0, 0), client_next=be.tick + 100,
                                            client_count=0)])
+            else:
+                for c in (3, 200, 4000):
+                    raw = be.read_nodes_raw(c, 1)
+                    lead = next(i for i in range(5) if raw[i].role == 2)
+                    if event == "node_term":           # a follower one term ahead
+                        raw[(lead + 1) % 5].current_term += 1
+                    else:                              # the leader's log gets a committed entry
+                        be.write_arena(c, lead + 1, [(raw[lead].current_term, 77)])
+                        raw[lead].log_len = 1
+                        raw[lead].commit_index = 1
+                        raw[lead].arena_base = 0
+                        raw[lead].arena_frontier = 1
+                    be.write_nodes(c, raw)
         for launch in range(10):
             g.step(1000)
             r.step(1000)
