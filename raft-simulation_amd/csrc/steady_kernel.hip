@@ -106,6 +106,110 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return __builtin_amdgcn_readlane(x, 63);
 }
 
+// A cluster at its fixed point, lane-resident: every follower took the leader's append-entries
+// (flags, votes, term and commit are what another one sets again), every response succeeded (next /
+// match / keys as another one sets them), the log is empty (a heartbeat ships nothing). With the
+// followers' re-armed timers (>= t_ae + el_base) unable to fire before the next round's
+// append-entries (el_base >= the round period P = 2d + F - 1 + hb) and the leader's responses all
+// before its next heartbeat (hb >= 2d + F), every round is the last one shifted by P: only the
+// ticks in the trace hashes change. Follower slot j is node j (j < L) or j + 1 (j >= L).
+template <int N>
+struct FixedPoint {
+  static constexpr int F = N - 1;
+  uint32_t L, Lid, Lterm, Lcommit;
+  uint64_t Ltr, ftr[F];
+  uint32_t Ldl, fdl[F], fpend;                       // fpend: followers whose draw is owed
+  uint32_t qmask, qA[F], qT[F], qa[F], qb[F];        // append-entries in flight, per follower
+  uint32_t rmask, resA, rT[F], rA[F], rB[F], rH[F];  // responses queued at the leader
+  uint32_t nhb, nae, nar;
+
+  __device__ __forceinline__ uint32_t fk(int j) const { return (uint32_t)j + ((uint32_t)j >= L ? 1u : 0u); }
+
+  // The append-entries of the round with heartbeat th reach every follower at ta = th + d.
+  __device__ __forceinline__ void append_entries(uint32_t ta, uint32_t d, uint32_t el_base) {
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER, Lterm, 0);
+      fdl[j] = ta + el_base;                          // + the owed draw
+      rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
+      qA[j] = INF;
+    }
+    fpend = (1u << F) - 1;
+    qmask = 0;
+    rmask = (1u << F) - 1;
+    resA = ta + d;
+    nae += F;
+  }
+  // The responses of the round with heartbeat th still queued, one per tick in slot order, up to
+  // tend - 1.
+  __device__ __forceinline__ void responses(uint32_t th, uint32_t tend, uint32_t d, uint32_t hb) {
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      const uint32_t tau = th + 2 * d + j;
+      if (((rmask >> j) & 1) && tau < tend) {
+        Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm, RAFT_LEADER,
+                          Lterm, 0);
+        rmask &= ~(1u << j);
+        Ldl = tau + hb;
+        ++nar;
+      }
+    }
+    if (!rmask) resA = INF;
+  }
+  // From the fixed point with the next heartbeat at th, every round to the launch's end: the rounds
+  // that end before it as trace hashes alone, then the one it cuts (heartbeat, append-entries and
+  // responses up to tend - 1; what is left stays queued as the general body leaves it). Every next
+  // event of the cluster is then at or after tend.
+  __device__ __forceinline__ void rounds(uint32_t th, uint32_t tend, uint32_t d, uint32_t hb,
+                                         uint32_t el_base) {
+    const uint32_t P = 2 * d + F - 1 + hb, last = 2 * d + F - 1;
+    const uint32_t K = tend > th + last ? (tend - th - last - 1) / P + 1 : 0;
+    const uint32_t tk = th + K * P;
+    if (K) {
+      // The trace hash is polynomial (device.hpp): a round's F + 1 leader events take the
+      // leader's hash h to h * M2^(F+1) + a, with a the Horner sum of the events' terms, and a
+      // round P ticks later adds P * M * (1 + M2 + ... + M2^F) to a; a follower's one event per
+      // round takes h to h * M2 + c, and c grows by P * M. One multiply-add per hash per round.
+      uint64_t a = trace_term(th, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        a = a * TRACE_M2 + trace_term(th + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
+                                      RAFT_LEADER, Lterm, 0);
+      const uint64_t da = (uint64_t)P * (TRACE_M * trace_geo<F + 1>());
+      const uint64_t df = (uint64_t)P * TRACE_M;
+      uint64_t cf = trace_term(th + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER, Lterm, 0);
+      for (uint32_t r = 0; r < K; ++r) {
+        Ltr = Ltr * trace_pow<F + 1>() + a;
+        a += da;
+#pragma unroll
+        for (int j = 0; j < F; ++j) ftr[j] = ftr[j] * TRACE_M2 + cf;
+        cf += df;
+      }
+#pragma unroll
+      for (int j = 0; j < F; ++j) fdl[j] = tk - P + d + el_base;   // + the owed draw
+      fpend = (1u << F) - 1;
+      Ldl = tk;                                   // = the last response + hb
+      nhb += K;
+      nae += F * K;
+      nar += F * K;
+    }
+    if (tk < tend) {                              // the round the launch's end cuts
+      Ltr = trace_event(Ltr, tk, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+      ++nhb;
+      Ldl = tk + hb;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        qA[j] = tk + d; qT[j] = Lterm; qa[j] = Lcommit; qb[j] = 0;
+      }
+      qmask = (1u << F) - 1;
+      if (tk + d < tend) {                        // the append-entries, then responses in time
+        append_entries(tk + d, d, el_base);
+        responses(tk, tend, d, hb);
+      }
+    }
+  }
+};
+
 template <int N>
 __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   static_assert(N >= 2 && N <= 5, "follower masks and the response queue fit four followers");
@@ -212,699 +316,817 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     }
   }
   const bool vouched = cert && !full;         // its lines past the second are the fixed point's
-#ifdef RS_WAVELOG
-  wl_loop = wall_clock64();
-#endif
-  auto field = [&](int f, uint32_t (&out)[N]) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) out[k] = w[HOT_CW + f * N + k];
-  };
-  uint32_t nfl[N], nqm[N];
-  field(HF_FLAGS, nfl);
-  field(HF_QMETA, nqm);
-  // exactly one leader; every node running; only the leader has leader-state
-  uint32_t L = 0, nlead = 0, badn = 0;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    const uint32_t f = nfl[k];
-    const bool lead = (f & 3) == RAFT_LEADER;
-    L = lead ? (uint32_t)k : L;
-    nlead += lead;
-    badn |= ((f >> 10) & 7) | (lead != (((f >> 14) & 1) != 0)) | (lead && (f & FL_DRAW));
-  }
-  bool bad = !active || nlead != 1 || badn != 0 || S.Q < (uint32_t)F;
-  const uint32_t Lid = L + 1;
-  // follower slot j is node j (j < L) or j + 1 (j >= L)
-  auto fsel = [&](const uint32_t (&v)[N], int j) { return msel((uint32_t)j >= L, v[j + 1], v[j]); };
-  auto fk = [&](int j) { return (uint32_t)j + ((uint32_t)j >= L ? 1u : 0u); };
-
-  uint32_t tmp[N];
-  // leader registers
-  const uint32_t Lfl = pick<N>(nfl, L);
-  field(HF_MASKS, tmp); uint32_t Lmk = pick<N>(tmp, L);
-  uint32_t fmk[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) fmk[j] = fsel(tmp, j);
-  field(HF_TERM, tmp); const uint32_t Lterm = pick<N>(tmp, L);
-  uint32_t fterm[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) fterm[j] = fsel(tmp, j);
-  field(HF_COMMIT, tmp); const uint32_t Lcommit = pick<N>(tmp, L);
-  uint32_t fcommit[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) fcommit[j] = fsel(tmp, j);
-  field(HF_LEN, tmp); const uint32_t Llen = pick<N>(tmp, L);
-  uint32_t flen[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) flen[j] = fsel(tmp, j);
-  field(HF_DEADLINE, tmp); uint32_t Ldl = pick<N>(tmp, L);
-  uint32_t fdl[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) fdl[j] = fsel(tmp, j);
-  uint32_t tlo[N], thi[N];
-  field(HF_TRACE_LO, tlo);
-  field(HF_TRACE_HI, thi);
-  uint64_t Ltr = (uint64_t)pick<N>(thi, L) << 32 | pick<N>(tlo, L);
-  uint64_t ftr[F];
-  uint32_t ffl[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) {
-    ftr[j] = (uint64_t)fsel(thi, j) << 32 | fsel(tlo, j);
-    ffl[j] = fsel(nfl, j);
-  }
-  // the leader's rows for its followers: next_index / match_index of peer id fk(j) + 1
-  int32_t nx[F], mt[F];
-  {
-    uint32_t rn[N], rm[N];                    // the leader's next / match of each peer id p + 1
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      field(HF_NEXT + p, tmp);
-      rn[p] = pick<N>(tmp, L);
-      field(HF_NEXT + N + p, tmp);
-      rm[p] = pick<N>(tmp, L);
-    }
-#pragma unroll
-    for (int j = 0; j < F; ++j) {
-      nx[j] = (int32_t)fsel(rn, j);
-      mt[j] = (int32_t)fsel(rm, j);
-    }
-  }
-  int32_t nx0[F], mt0[F];                     // as loaded: unchanged words are not stored back
-#pragma unroll
-  for (int j = 0; j < F; ++j) {
-    nx0[j] = nx[j];
-    mt0[j] = mt[j];
-  }
-  const bool ackbad = Llen > w[CLW];          // a success response would be checker work (P4)
-  const uint32_t Lkeys = Lmk >> 16;
-  // heartbeats need full leader-state, no LazySeq log and commit within the log
-  // (append-entries-rpc's IOOBE/NPE/CCE checks, core.clj:56-67): constant over the launch
-  bad = bad || (Lkeys & (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid))) !=
-                   (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid)) ||
-        ((Lfl >> 13) & 1) || Lcommit > Llen;
-
-  // ---------------------------------------------------------------- queued messages
-  uint32_t qmask = 0, rmask = 0, resA = INF;
-  uint32_t qA[F], qT[F], qa[F], qb[F], rT[F], rA[F], rB[F], rH[F];
-#pragma unroll
-  for (int j = 0; j < F; ++j) {
-    qA[j] = INF; qT[j] = qa[j] = qb[j] = 0;
-    rT[j] = rA[j] = rB[j] = rH[j] = 0;
-  }
-  if (!bad) {
-    const uint32_t Lqm = pick<N>(nqm, L);
-    bad = (Lqm >> 4) & 31;                                   // the leader's REQ queue is empty
-    const uint32_t rsh = (Lqm >> 9) & 15, rsc = (Lqm >> 13) & 31;
-    uint32_t need = 0, rqh[F];
-#pragma unroll
-    for (int j = 0; j < F; ++j) {
-      const uint32_t qm = fsel(nqm, j);
-      const uint32_t rqc = (qm >> 4) & 31;
-      rqh[j] = qm & 15;
-      bad = bad || rqc > 1 || ((qm >> 13) & 31) != 0;       // <= 1 request, no responses
-      need |= (uint32_t)(rqc != 0) << j;
-    }
-    bad = bad || rsc > (uint32_t)F;
-    // The messages: loaded by every lane of a wave in which any lane has one (a message in flight
-    // at the launch's start is rare), all loads issued before any is looked at -- one memory round
-    // trip, where loads under per-lane branches each waited for the last. Slot indices are
-    // clamped into the ring for lanes whose queue words are not looked at.
-    uint4 qm0[F], qm1[F], rm0[F], rm1[F];
-    if (__builtin_amdgcn_ballot_w64(!bad && (need || rsc))) {     // wave-uniform
-#pragma unroll
-      for (int j = 0; j < F; ++j) {                          // the leader's append-entries
-        const uint4* mp = reinterpret_cast<const uint4*>(
-            qslots(S, c * N + fk(j), 0) + min(rqh[j], S.Q - 1) * qstride(S, 0));
-        qm0[j] = mp[0];
-        qm1[j] = mp[1];
-      }
-#pragma unroll
-      for (int i = 0; i < F; ++i) {                          // append-responses, sender order
-        const uint4* mp = reinterpret_cast<const uint4*>(
-            qslots(S, c * N + L, 1) + min(wrapq(rsh + i, S.Q), S.Q - 1) * qstride(S, 1));
-        rm0[i] = mp[0];
-        rm1[i] = mp[1];
-      }
-    }
-    if (!bad) {
-#pragma unroll
-      for (int j = 0; j < F; ++j) {
-        if ((need >> j) & 1) {
-          const uint4 m0 = qm0[j], m1 = qm1[j];
-          bad = bad || m0.y != (RAFT_MSG_APPEND_ENTRIES | Lid << 3) || m1.y || m1.z || m1.w;
-          qmask |= 1u << j;
-          qA[j] = m0.x; qT[j] = m0.z; qa[j] = m0.w; qb[j] = m1.x;
-        }
-      }
-      uint32_t last = 0;
-#pragma unroll
-      for (int i = 0; i < F; ++i) {
-        if ((uint32_t)i < rsc && !bad) {
-          const uint4 m0 = rm0[i], m1 = rm1[i];
-          const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
-          bad = (hdr & 7) != RAFT_MSG_APPEND_RESPONSE || (hdr >> 8) || m1.y || m1.z || m1.w ||
-                src <= last || src > (uint32_t)N || src == Lid || (i && m0.x != resA);
-          last = src;
-          resA = m0.x;
-          const uint32_t j = src - 1 - (src > Lid ? 1u : 0u);
-          if (!bad) {
-            rmask |= 1u << j;
-#pragma unroll
-            for (int jj = 0; jj < F; ++jj) {
-              if ((uint32_t)jj == j) {
-                rT[jj] = m0.z; rA[jj] = m0.w; rB[jj] = m1.x; rH[jj] = (hdr >> 7) & 1;
-              }
-            }
-          }
-        }
-      }
-    }
-    if (!rmask) resA = INF;
-  }
-  record_bail(active && bad, t0);           // outside the model from the start: bail at t0
-  bool wb = active && !bad;
-  bool run = wb;
-
-  // ---------------------------------------------------------------- the cluster's ticks
   const uint32_t tend = t0 + nt, d = S.dmin;
-  uint32_t tn = t0, nhb = 0, nae = 0, nar = 0;
-  // followers whose deadline holds its lower bound t_ae + el_base (the draw is deferred)
-  // (a draw owed from an earlier launch: FL_DRAW in the follower's flags, device.hpp)
-  uint32_t fpend = 0;
-#pragma unroll
-  for (int j = 0; j < F; ++j) fpend |= ((ffl[j] & FL_DRAW) ? 1u : 0u) << j;
-  auto draw_deadlines = [&](uint32_t due) {
-#pragma unroll
-    for (int j = 0; j < F; ++j) {
-      if ((due >> j) & 1) {
-        const uint4 wd = event_draw(g, fk(j) + 1, fdl[j] - S.el_base, S);   // D4, core.clj:174
-        fdl[j] += __umulhi(wd.y, S.el_span);
-      }
-    }
-    fpend &= ~due;
-  };
-  auto next_event = [&]() {
-    uint32_t m = min(Ldl, resA);
-#pragma unroll
-    for (int j = 0; j < F; ++j) m = min(m, min(fdl[j], qA[j]));
-    return m;
-  };
-  const uint32_t P = 2 * d + F - 1 + S.hb, last = 2 * d + F - 1, allF = (1u << F) - 1;
-  // The cluster at its fixed point: every follower took the leader's append-entries (flags,
-  // votes, term and commit are what another one sets again), every response succeeded (next /
-  // match / keys as another one sets them), the log is empty (a heartbeat ships nothing) and no
-  // message is in flight. If the followers' re-armed timers (>= t_ae + el_base) cannot fire
-  // before the next round's append-entries (el_base >= the round period P) and the leader's
-  // responses all fit before its next heartbeat (hb >= 2d + F), every later round is this one
-  // shifted by a multiple of P: only the ticks in the trace hashes change.
-  auto at_fixed_point_state = [&]() {
-    bool ok = Llen == 0 && !ackbad;
-#pragma unroll
-    for (int j = 0; j < F; ++j)
-      ok = ok && fterm[j] == Lterm &&
-           (ffl[j] & (3u | 15u << 2 | 15u << 6 | 1u << 13)) == (RAFT_FOLLWER | Lid << 6) &&
-           fcommit[j] == flen[j] && (fmk[j] & 0xFFFFu) == 0 && nx[j] == 0 &&
-           mt[j] == (int32_t)Lcommit;
-    return ok;
-  };
-  auto at_fixed_point = [&]() {
-    return S.el_base >= P && S.hb >= 2 * d + F && !qmask && !rmask && at_fixed_point_state();
-  };
-  // From the fixed point with the next heartbeat at th, every round to the launch's end as trace
-  // hashes: the rounds that end before it, then the one it cuts (heartbeat, append-entries and
-  // responses up to tend - 1; what is left is queued as the general body leaves it): every next
-  // event of the cluster is then at or after tend.
-  auto fixed_point_rounds = [&](uint32_t th) {
-    const uint32_t K = tend > th + last ? (tend - th - last - 1) / P + 1 : 0;
-    uint32_t tk = th + K * P;
-    if (K) {
-      // The trace hash is polynomial (device.hpp): a round's F + 1 leader events take the
-      // leader's hash h to h * M2^(F+1) + a, with a the Horner sum of the events' terms, and a
-      // round P ticks later adds P * M * (1 + M2 + ... + M2^F) to a; a follower's one event per
-      // round takes h to h * M2 + c, and c grows by P * M. One multiply-add per hash per round.
-      uint64_t a = trace_term(th, 7, 0, 0, RAFT_LEADER, Lterm, 0);
-#pragma unroll
-      for (int j = 0; j < F; ++j)
-        a = a * TRACE_M2 + trace_term(th + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
-                                      RAFT_LEADER, Lterm, 0);
-      const uint64_t da = (uint64_t)P * (TRACE_M * trace_geo<F + 1>());
-      const uint64_t df = (uint64_t)P * TRACE_M;
-      uint64_t cf[F];
-#pragma unroll
-      for (int j = 0; j < F; ++j)
-        cf[j] = trace_term(th + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER, Lterm, 0);
-      for (uint32_t r = 0; r < K; ++r) {
-        Ltr = Ltr * trace_pow<F + 1>() + a;
-        a += da;
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          ftr[j] = ftr[j] * TRACE_M2 + cf[j];
-          cf[j] += df;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < F; ++j) fdl[j] = tk - P + d + S.el_base;   // + the deferred draw
-      fpend = (1u << F) - 1;
-      Ldl = tk;                                   // = the last response + hb
-      nhb += K;
-      nae += F * K;
-      nar += F * K;
-    }
-    if (tk < tend) {                              // the round the launch's end cuts
-      Ltr = trace_event(Ltr, tk, 7, 0, 0, RAFT_LEADER, Lterm, 0);
-      ++nhb;
-      Ldl = tk + S.hb;
-#pragma unroll
-      for (int j = 0; j < F; ++j) {
-        qA[j] = tk + d; qT[j] = Lterm; qa[j] = Lcommit; qb[j] = 0;
-      }
-      qmask = (1u << F) - 1;
-      if (tk + d < tend) {                        // the append-entries, then responses in time
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          ftr[j] = trace_event(ftr[j], tk + d, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
-                               Lterm, 0);
-          fdl[j] = tk + d + S.el_base;
-          rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
-          qA[j] = INF;
-        }
-        fpend = (1u << F) - 1;
-        qmask = 0;
-        rmask = (1u << F) - 1;
-        resA = tk + 2 * d;
-        nae += F;
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          if (tk + 2 * d + j < tend) {
-            Ltr = trace_event(Ltr, tk + 2 * d + j, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm,
-                              RAFT_LEADER, Lterm, 0);
-            rmask &= ~(1u << j);
-            Ldl = tk + 2 * d + j + S.hb;
-            ++nar;
-          }
-        }
-      }
-    }
-  };
+  const uint32_t P = 2 * d + F - 1 + S.hb, allF = (1u << F) - 1;
+  uint32_t dl = 0, nhb = 0, nae = 0, nar = 0;  // lines of the block changed; events run
+#ifdef RS_WAVELOG
+  uint64_t wl_x1 = 0, wl_x2 = 0, wl_x3 = 0, wl_lend = 0;
+#endif
 
-  // ------------------------------------------- the fixed-point path (C2's steady state)
-  // A cluster at its fixed point (above) whose round in progress at t0 is on the period-P
-  // schedule -- none (the next heartbeat at Ldl >= t0), its append-entries in flight, or its
-  // responses pending exactly as the last launch's end cut them -- and whose followers' timers
-  // cannot fire before their next append-entries runs every event of the launch here: the rest
-  // of that round event by event, then fixed_point_rounds. Everything else is the general loop's.
-  bool fp = wb && S.el_base >= P && S.hb >= 2 * d + F && (vouched || at_fixed_point_state());
-  uint32_t th0 = Ldl, mid = 0;               // the round's heartbeat; 1 AEs in flight, 2 responses
-  if (qmask) {
-    mid = 1;
-    th0 = qA[0] - d;
-    fp = fp && qmask == allF && !rmask && qA[0] >= t0 && qA[0] >= d && Ldl == th0 + S.hb;
-#pragma unroll
-    for (int j = 0; j < F; ++j)
-      fp = fp && qA[j] == qA[0] && qT[j] == Lterm && qa[j] == Lcommit && qb[j] == 0;
-  } else if (rmask) {
-    mid = 2;
-    th0 = resA - 2 * d;
-    const uint32_t j0 = (uint32_t)F - __popc(rmask);          // responses already taken
-    const int64_t cut = (int64_t)t0 - ((int64_t)th0 + 2 * d);  // what the last launch's end cut
-    fp = fp && resA >= 2 * d && rmask == (allF & ~((1u << j0) - 1)) &&
-         (int64_t)j0 == (cut < 0 ? 0 : cut > F ? (int64_t)F : cut) &&
-         Ldl == (j0 ? th0 + 2 * d + j0 - 1 : th0) + S.hb;
-#pragma unroll
-    for (int j = 0; j < F; ++j)
-      fp = fp && (!((rmask >> j) & 1) ||
-                  (rT[j] == Lterm && rA[j] == Lcommit && rB[j] == 0 && rH[j] == 1));
-  } else {
-    fp = fp && Ldl >= t0;
-  }
+  // ------------------------------------------- the certified path
+  // A wave whose every cluster is vouched for by its certificate (device.hpp), on the fixed
+  // point's period-P schedule (its round in progress at t0: none, the append-entries in flight, or
+  // the responses the last launch's end cut) and with its followers' draws owed (FL_DRAW) runs the
+  // whole launch from the first two lines of its blocks: the rest of that round, then
+  // FixedPoint::rounds. Queued messages are not read: a certified cluster's are the fixed point's
+  // (whatever else writes a ring clears the certificate), and so are its leader's commit (0) and
+  // the rest of its state. Any other wave takes the general path below.
+  FixedPoint<N> fx;
+  uint32_t lmid = 0, lth0 = 0;
+  bool lean = vouched && S.el_base >= P && S.hb >= 2 * d + F && S.Q >= (uint32_t)F;
   {
-    const uint32_t nxt = min((mid == 2 ? th0 + P : th0) + d, tend);   // the next AE (or the end)
+    const uint32_t L = Lc;
+    auto lw = [&](int f, int k) { return w[HOT_CW + f * N + k]; };
+    auto lpick = [&](int f) {                       // field f of the leader
+      uint32_t v = 0;
 #pragma unroll
-    for (int j = 0; j < F; ++j) fp = fp && fdl[j] >= nxt;
-  }
-  // A vouched cluster off the fixed-point path (set_tick moved the clock, ...) has no full state
-  // here: the general body runs it from t0.
-  const bool vbail = vouched && wb && !fp;
-  record_bail(vbail, t0);
-  if (vbail) wb = run = false;
-  if (fp) {
-    run = false;
-    bool whole = true;                        // the round in progress finished in this launch
-    if (mid == 1) {
-      const uint32_t ta = qA[0];
-      if (ta < tend) {                        // the append-entries
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
-                               Lterm, 0);
-          fdl[j] = ta + S.el_base;
-          qA[j] = INF;
-          rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
-        }
-        fpend = allF;
-        qmask = 0;
-        rmask = allF;
-        resA = ta + d;
-        nae += F;
-      } else {
-        whole = false;
-      }
-    }
-    if (mid && whole) {                       // the responses, one per tick in slot order
-#pragma unroll
-      for (int j = 0; j < F; ++j) {
-        const uint32_t tau = th0 + 2 * d + j;
-        if (((rmask >> j) & 1) && tau < tend) {
-          Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm, RAFT_LEADER,
-                            Lterm, 0);
-          rmask &= ~(1u << j);
-          Ldl = tau + S.hb;
-          ++nar;
-        }
-      }
-      if (rmask) whole = false;
-      else resA = INF;
-    }
-    if (whole) fixed_point_rounds(mid ? th0 + P : th0);
-  }
-#ifdef RS_WAVELOG
-  wl_ts = __builtin_amdgcn_s_memtime();
-#endif
-  bool pbail = false;                        // bailed in the last trip, not yet recorded
-  uint32_t pbt = 0;
-  for (;;) {
-    record_bail(pbail, pbt);                 // the loop's head: every lane active
-    pbail = false;
-    uint32_t t = max(tn, next_event());
-    // a deferred deadline at or before the tick to decide is drawn first (it can only move later)
-    for (;;) {
-      uint32_t due = 0;
-#pragma unroll
-      for (int j = 0; j < F; ++j) due |= (uint32_t)(fdl[j] <= t) << j;
-      due &= fpend;
-      if (!run || t >= tend || !due) break;
-      draw_deadlines(due);
-      t = max(tn, next_event());
-    }
-    const bool on = run && t < tend;
-    if (!__builtin_amdgcn_ballot_w64(on)) break;
-#ifdef RS_WAVELOG
-    if (!wl_trips) wl_first = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(on));
-    ++wl_trips;
-#endif
-    RS_LPH(0);
-    if (!on) continue;
-    // ------------------------------------------------ decide on the pre-tick state
-    const bool lres = rmask != 0 && resA <= t;               // a message beats the deadline
-    const bool lhb = !lres && Ldl <= t;
-    uint32_t fae = 0, fto = 0;
+      for (int k = 0; k < N; ++k) v |= lw(f, k) & (0u - (uint32_t)(L == (uint32_t)k));
+      return v;
+    };
+    auto lfol = [&](int f, int j) {                 // field f of follower slot j
+      const uint32_t m = 0u - (uint32_t)((uint32_t)j >= L);
+      return (lw(f, j + 1) & m) | (lw(f, j) & ~m);
+    };
+    fx.L = L; fx.Lid = L + 1; fx.Lterm = lpick(HF_TERM); fx.Lcommit = 0;
+    fx.Ldl = lpick(HF_DEADLINE);
+    fx.Ltr = (uint64_t)lpick(HF_TRACE_HI) << 32 | lpick(HF_TRACE_LO);
+    fx.qmask = fx.rmask = 0; fx.resA = INF; fx.fpend = allF; fx.nhb = fx.nae = fx.nar = 0;
+    const uint32_t Lqm = lpick(HF_QMETA);
+    const uint32_t rsc = (Lqm >> 13) & 31;
+    uint32_t need = 0;
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      const bool a = qA[j] <= t;
-      fae |= (uint32_t)a << j;
-      fto |= (uint32_t)(!a && fdl[j] <= t) << j;
+      fx.fdl[j] = lfol(HF_DEADLINE, j);
+      fx.ftr[j] = (uint64_t)lfol(HF_TRACE_HI, j) << 32 | lfol(HF_TRACE_LO, j);
+      const uint32_t qm = lfol(HF_QMETA, j);
+      lean = lean && (lfol(HF_FLAGS, j) & FL_DRAW) && ((qm >> 4) & 31) <= 1 && !((qm >> 13) & 31);
+      need |= (((qm >> 4) & 31) ? 1u : 0u) << j;
+      fx.qA[j] = INF; fx.qT[j] = fx.qa[j] = fx.qb[j] = 0;
+      fx.rT[j] = fx.rA[j] = fx.rB[j] = fx.rH[j] = 0;
     }
-    bool bail = fto != 0;                                    // a follower's election timeout
-    if (lhb) {
-      bail = bail || qmask != 0;                             // a follower still holds one
+    lean = lean && !((Lqm >> 4) & 31) && rsc <= (uint32_t)F && !(need && rsc) &&
+           (need == 0 || need == allF);
+    lth0 = fx.Ldl;
+    if (need) {                                     // the append-entries in flight
+      lmid = 1;
+      const uint32_t ta = lfol(HF_REQ_ARR, 0);
+      lth0 = ta - d;
+      lean = lean && ta >= t0 && ta >= d && fx.Ldl == lth0 + S.hb;
 #pragma unroll
       for (int j = 0; j < F; ++j) {
-        const uint32_t pv = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
-        bail = bail || pv < Llen || pv >= (1u << 24);        // entries to ship
+        lean = lean && lfol(HF_REQ_ARR, j) == ta;
+        fx.qA[j] = ta; fx.qT[j] = fx.Lterm;
       }
-    }
-    const int hs = __builtin_ctz(rmask | (1u << F));
-    uint32_t xT = 0, xH = 0;
-#pragma unroll
-    for (int j = 0; j < F; ++j) {
-      if (j == hs) {
-        xT = rT[j]; xH = rH[j];
-      }
-    }
-    const uint32_t xid = (uint32_t)hs + 1 + ((uint32_t)hs >= L ? 1u : 0u);
-    if (lres)
-      bail = bail || xT > Lterm || (xH ? ackbad : ((Lmk >> (16 + xid)) & 1) == 0);
-    if (fae) {
-      bail = bail || rmask != 0;                             // responses of two ticks
-#pragma unroll
-      for (int j = 0; j < F; ++j)
-        if ((fae >> j) & 1)
-          bail = bail || qb[j] != 0 || !(qT[j] < fterm[j] || flen[j] <= fcommit[j]);
-    }
-    RS_LPH(1);
-    if (bail) {                              // the general tick body runs this tick
-      pbail = true;
-      pbt = t;
-      run = false;
-      continue;
-    }
-    // ------------------------------------------------ run
-    uint32_t tl = t;                         // the last tick run (a round or a drain runs more)
-    bool round = false;
-    if (lhb) {                               // heartbeat-handler: empty append-entries to all
+      fx.qmask = allF;
+    } else if (rsc) {                               // the responses the last launch's end cut
+      lmid = 2;
+      const uint32_t ra = lpick(HF_RES_ARR), j0 = (uint32_t)F - rsc;
+      lth0 = ra - 2 * d;
+      const int64_t cut = (int64_t)t0 - ((int64_t)lth0 + 2 * d);
+      lean = lean && ra >= 2 * d && (int64_t)j0 == (cut < 0 ? 0 : cut > F ? (int64_t)F : cut) &&
+             fx.Ldl == (j0 ? lth0 + 2 * d + j0 - 1 : lth0) + S.hb;
+      fx.rmask = allF & ~((1u << j0) - 1);
+      fx.resA = ra;
 #pragma unroll
       for (int j = 0; j < F; ++j) {
-        qA[j] = t + d; qT[j] = Lterm; qa[j] = Lcommit;
-        qb[j] = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
+        fx.rT[j] = fx.Lterm; fx.rH[j] = 1;
       }
-      qmask = (1u << F) - 1;
-      Ldl = t + S.hb;
-      Ltr = trace_event(Ltr, t, 7, 0, 0, RAFT_LEADER, Lterm, 0);
-      ++nhb;
-      // The whole heartbeat round in this trip when nothing else can happen before its last
-      // response: every follower takes the append-entries at t + d (no follower deadline before
-      // it; the handler's checks pass), the followers' re-armed deadlines (>= t + d + el_base) and
-      // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the
-      // append-entries come before the launch ends (and no older response is still queued). The
-      // responses then run in slot order up to the launch end (the rest stay queued) and stop at
-      // one outside the model (the next trip decides it). A deferred deadline counts with its
-      // lower bound here (a round not taken is run tick by tick).
-      round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > d;
-#pragma unroll
-      for (int j = 0; j < F; ++j)
-        round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
+    } else {
+      lean = lean && fx.Ldl >= t0;
     }
-    RS_LPH(2);
-    // A trip runs exactly one of: a whole round (below), a heartbeat alone (its round did not fit:
-    // the append-entries are taken one tick later as `fae`), append-entries that arrived (fae),
-    // or queued responses (lres): a heartbeat with a follower still holding an append-entries,
-    // and append-entries with responses still queued, were bailed above.
-    auto append_entries = [&](uint32_t ta, uint32_t fa) {   // append-entries-handler, followers fa
+    const uint32_t nxt = min((lmid == 2 ? lth0 + P : lth0) + d, tend);   // the next AE (or end)
 #pragma unroll
-      for (int j = 0; j < F; ++j) {
-        if ((fa >> j) & 1) {
-          const uint32_t mterm = qT[j], rterm = fterm[j];
-          const bool ok = mterm >= fterm[j];
-          const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) |
-                                         RAFT_FOLLWER | Lid << 6
-                                   : ffl[j];
-          const uint32_t nterm = ok ? mterm : fterm[j];
-          ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3, nterm, 0);
-          if (ok) {
-            fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
-            fmk[j] &= 0xFFFF0000u;
-          }
-          fterm[j] = nterm;
-          ffl[j] = nfl2;
-          // the response: to the leader's RES queue, in sender id order
-          rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
-          qA[j] = INF;
-          fdl[j] = ta + S.el_base;                           // + the deferred draw
-        }
-      }
-      fpend |= fa;
-      qmask &= ~fa;
-      rmask = fa;
-      resA = ta + d;
-      nae += __popc(fa);
-      tl = ta;
-    };
-    // append-response-handler for follower slot j's response at tick tau (core.clj:141-149);
-    // false (and nothing done) when it is outside the model: a newer term, a success response
-    // that would be checker work, or a failure without the peer's key (NPE)
-    auto response = [&](int j, uint32_t tau, uint32_t yT, uint32_t yA, uint32_t yB, uint32_t yH,
-                        int32_t& nxj, int32_t& mtj) {
-      const uint32_t yid = fk(j) + 1;
-      if (yT > Lterm || (yH ? ackbad : ((Lmk >> (16 + yid)) & 1) == 0)) return false;
-      rmask &= ~(1u << j);
-      Lmk |= yH << (16 + yid);
-      nxj = yH ? (int32_t)yB : nxj - 1;
-      mtj = yH ? (int32_t)yA : mtj;
-      Ldl = tau + S.hb;
-      Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, yid, yT, RAFT_LEADER, Lterm, 0);
-      ++nar;
-      tl = tau;
-      return true;
-    };
-    if (round) {
-      // every follower at t + d, then the responses at t + 2d .. t + 2d + F - 1 in slot order (the
-      // round's conditions put them all before the launch end and every follower's next event):
-      // straight-line code, every index static
-      append_entries(t + d, (1u << F) - 1);
-      bool go = true;
-#pragma unroll
-      for (int j = 0; j < F; ++j)     // (a round cut by the launch end leaves the rest queued)
-        go = go && t + 2 * d + j < tend &&
-             response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
-      if (!rmask) resA = INF;
-      if (at_fixed_point()) {
-        fixed_point_rounds(t + P);
-        tl = tend - 1;                       // nothing of the cluster is left before tend
-      }
-    } else if (fae || lres) {
-      // fae: the append-entries at t, then their responses from t + d in the same trip unless
-      // the leader's heartbeat falls due before them. The responses run one per tick, heads in
-      // sender order, while nothing else in the cluster is due (the followers' next events and
-      // the launch end; the leader's own deadline moves past each); lres: the first one at t
-      // was decided above. A response outside the model ends the run and the next trip
-      // decides it. A round finished here (one the last launch cut) continues at the fixed point.
-      uint32_t tau0 = t;
-      if (fae) {
-        append_entries(t, fae);
-        tau0 = Ldl >= t + d ? t + d : tend;
-      }
-      uint32_t E = tend;
-#pragma unroll
-      for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
-      if (lres) E = max(E, t + 1);
-      for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
-        const int h2 = __builtin_ctz(rmask);
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < F; ++j)
-          if (j == h2) ok = response(j, tau, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
-        if (!ok) break;
-        if (!rmask) resA = INF;
-      }
-      if (at_fixed_point() && Ldl > tl) {
-        fixed_point_rounds(Ldl);
-        tl = tend - 1;
-      }
-    }
-    RS_LPH(4);
-    tn = tl + 1;
+    for (int j = 0; j < F; ++j) lean = lean && fx.fdl[j] >= nxt;
   }
-  // the draws still owed stay owed in the stored state (FL_DRAW): a cluster at its fixed point
-  // makes none at all
-
-#ifdef RS_WAVELOG
-  const uint64_t wl_lend = wall_clock64();
-  const uint32_t wl_events = nhb + nae + nar;
-#endif
-  // ---------------------------------------------------------------- write back
-  if (S.shist) {
-    // packing key for the next launch (bailed clusters get theirs from the catch-up below); the
-    // wave's clusters share a few keys: one histogram atomic per distinct key
-    const bool kl = wb && run;
-    const uint32_t key = kl ? sched_bucket(next_event(), tend) : INF;
-    if (kl) S.skey[c] = key;
-    uint64_t pend = __builtin_amdgcn_ballot_w64(kl);
-    while (pend) {
-      const uint32_t k = (uint32_t)__shfl((int)key, (int)__builtin_ctzll(pend));
-      const uint64_t same = __builtin_amdgcn_ballot_w64(kl && key == k);
-      if (lane == (uint32_t)__builtin_ctzll(pend)) atomicAdd(&S.shist[k], (uint32_t)__popcll(same));
-      pend &= ~same;
-    }
-  }
-  uint32_t dl = 0;                           // lines of the cluster's block changed
-  const bool wfp = !__builtin_amdgcn_ballot_w64(wb && !fp);
-  if (wb) {
-    // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
-    constexpr int NV = HF_NEXT;
-    uint32_t v[NV][N];
+  const bool lean_wave = !__builtin_amdgcn_ballot_w64(active && !lean);     // uniform
+  bool wb = false;
+  if (lean_wave) {
+    if (active) {
+      bool whole = true;                      // the round in progress finished in this launch
+      if (lmid == 1) {
+        if (fx.qA[0] < tend) fx.append_entries(fx.qA[0], d, S.el_base);
+        else whole = false;
+      }
+      if (lmid && whole) {
+        fx.responses(lth0, tend, d, S.hb);
+        whole = !fx.rmask;
+      }
+      if (whole) fx.rounds(lmid ? lth0 + P : lth0, tend, d, S.hb, S.el_base);
+      nhb = fx.nhb; nae = fx.nae; nar = fx.nar;
+      // fields DEADLINE .. RES_TAIL of every node back into the image (the rest is unchanged)
+      const uint32_t L = fx.L;
+      uint32_t v[HF_FLAGS][N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-      // node k is the leader (k == L) or follower slot k - 1 (k > L) / k (k < L)
-      const bool isL = (uint32_t)k == L;
-      const int jl = k > 0 ? k - 1 : 0, jh = k < F ? k : F - 1;
-      const bool lo = (uint32_t)k > L;
-      auto fv = [&](const uint32_t* x) { return msel(lo, x[jl], x[jh]); };
-      const uint32_t fq = (qmask >> (lo ? jl : jh)) & 1;
-      const uint32_t fqa = fv(qA);
-      const uint64_t trf = (uint64_t)msel(lo, (uint32_t)(ftr[jl] >> 32), (uint32_t)(ftr[jh] >> 32)) << 32 |
-                          msel(lo, (uint32_t)ftr[jl], (uint32_t)ftr[jh]);
-      const uint64_t tr = isL ? Ltr : trf;
-      v[HF_FLAGS][k] = isL ? Lfl : (fv(ffl) & ~FL_DRAW) | (((fpend >> (lo ? jl : jh)) & 1) ? FL_DRAW : 0u);
-      v[HF_MASKS][k] = isL ? Lmk : fv(fmk);
-      v[HF_TERM][k] = isL ? Lterm : fv(fterm);
-      v[HF_COMMIT][k] = isL ? Lcommit : fv(fcommit);
-      v[HF_LEN][k] = isL ? Llen : fv(flen);
-      v[HF_DEADLINE][k] = isL ? Ldl : fv(fdl);
-      v[HF_QMETA][k] = isL ? pack_qmeta(0, 0, 0, __popc(rmask)) : pack_qmeta(0, fq, 0, 0);
-      v[HF_REQ_ARR][k] = isL ? INF : (fq ? fqa : INF);
-      v[HF_RES_ARR][k] = isL ? resA : INF;
-      v[HF_REQ_TAIL][k] = isL ? 0u : (fq ? fqa : 0u);
-      v[HF_RES_TAIL][k] = isL ? (rmask ? resA : 0u) : 0u;
-      v[HF_TRACE_LO][k] = (uint32_t)tr;
-      v[HF_TRACE_HI][k] = (uint32_t)(tr >> 32);
-    }
-    auto live = [](int q) { return q >= (int)HOT_CW && q < (int)(HOT_CW + HF_NEXT * N); };
-    auto val = [&](int q) { return v[(q - HOT_CW) / N][(q - HOT_CW) % N]; };
-    // The changed chunks into the image (in a heartbeat round the deadlines and trace hashes
-    // change, all in the block's first line; flags, terms, masks, commits, queue words and rows
-    // come back unchanged); the lines they dirty go back to memory whole, below.
-    // A wave whose written-back clusters all took the fixed-point path changed nothing past the
-    // queue words and the flags' FL_DRAW (masks, terms, commits, lengths and rows are the fixed
-    // point's).
-    const int ch_end = wfp ? (int)(HOT_CW + (HF_FLAGS + 1) * N + 3) / 4
-                           : (int)(HOT_CW + HF_NEXT * N + 3) / 4;
-    // (every chunk is written back to the image, changed or not: no branch per chunk)
+      for (int k = 0; k < N; ++k) {
+        const bool isL = (uint32_t)k == L;
+        const int jl = k > 0 ? k - 1 : 0, jh = k < F ? k : F - 1;
+        const bool lo = (uint32_t)k > L;
+        auto fv = [&](const uint32_t* x) { return msel(lo, x[jl], x[jh]); };
+        const uint32_t fq = (fx.qmask >> (lo ? jl : jh)) & 1, fqa = fv(fx.qA);
+        const uint64_t trf = (uint64_t)msel(lo, (uint32_t)(fx.ftr[jl] >> 32),
+                                            (uint32_t)(fx.ftr[jh] >> 32)) << 32 |
+                             msel(lo, (uint32_t)fx.ftr[jl], (uint32_t)fx.ftr[jh]);
+        const uint64_t tr = isL ? fx.Ltr : trf;
+        v[HF_DEADLINE][k] = isL ? fx.Ldl : fv(fx.fdl);
+        v[HF_TRACE_LO][k] = (uint32_t)tr;
+        v[HF_TRACE_HI][k] = (uint32_t)(tr >> 32);
+        v[HF_QMETA][k] = isL ? pack_qmeta(0, 0, 0, __popc(fx.rmask)) : pack_qmeta(0, fq, 0, 0);
+        v[HF_REQ_ARR][k] = isL ? INF : (fq ? fqa : INF);
+        v[HF_RES_ARR][k] = isL ? fx.resA : INF;
+        v[HF_REQ_TAIL][k] = isL ? 0u : (fq ? fqa : 0u);
+        v[HF_RES_TAIL][k] = isL ? (fx.rmask ? fx.resA : 0u) : 0u;
+      }
+      auto in = [](int q) { return q >= (int)HOT_CW && q < (int)(HOT_CW + HF_FLAGS * N); };
+      auto val = [&](int q) { return v[(q - HOT_CW) / N][(q - HOT_CW) % N]; };
 #pragma unroll
-    for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_NEXT * N + 3) / 4; ++i) {
-      if (i < ch_end) {                                    // wave-uniform
+      for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_FLAGS * N + 3) / 4; ++i) {
         const int q = 4 * i;
-        const uint4 x = make_uint4(live(q) ? val(q) : w[q], live(q + 1) ? val(q + 1) : w[q + 1],
-                                   live(q + 2) ? val(q + 2) : w[q + 2],
-                                   live(q + 3) ? val(q + 3) : w[q + 3]);
+        const uint4 x = make_uint4(in(q) ? val(q) : w[q], in(q + 1) ? val(q + 1) : w[q + 1],
+                                   in(q + 2) ? val(q + 2) : w[q + 2],
+                                   in(q + 3) ? val(q + 3) : w[q + 3]);
         *lds_at<uint4>(img, img_off(lane, i)) = x;
         dl |= (uint32_t)(x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3])
               << (i / 8);
       }
     }
-    // the steady certificate for the next launch: the cluster stays at its fixed point
-    const uint32_t cn = fp || (full && at_fixed_point_state()) ? (CERT_MAGIC | L) : 0u;
-    *lds_at<uint4>(img, img_off(lane, CL_CERT / 4)) = make_uint4(w[4], w[5], w[6], cn);
-    dl |= (uint32_t)(cn != w[CL_CERT]);
-    // the leader's rows (node L): next / match of peer fk(j) + 1
-    if (!wfp) {
+    // messages in flight at the launch's end back to the rings, heads at slot 0 (rare)
+    if (__builtin_amdgcn_ballot_w64(active && (fx.qmask || fx.rmask))) {   // wave-uniform
 #pragma unroll
       for (int j = 0; j < F; ++j) {
-        const uint32_t qn = HOT_CW + (HF_NEXT + fk(j)) * N + L;
-        const uint32_t qt = HOT_CW + (HF_NEXT + N + fk(j)) * N + L;
-        if (nx[j] != nx0[j]) {
-          *lds_at<uint32_t>(img, img_off(lane, qn / 4) + 4 * (qn % 4)) = (uint32_t)nx[j];
-          dl |= 1u << (qn / 32);
-        }
-        if (mt[j] != mt0[j]) {
-          *lds_at<uint32_t>(img, img_off(lane, qt / 4) + 4 * (qt % 4)) = (uint32_t)mt[j];
-          dl |= 1u << (qt / 32);
+        if (active && ((fx.qmask >> j) & 1)) {
+          uint4* dp = reinterpret_cast<uint4*>(qslots(S, c * N + fx.fk(j), 0));
+          dp[0] = make_uint4(fx.qA[j], RAFT_MSG_APPEND_ENTRIES | fx.Lid << 3, fx.qT[j], fx.qa[j]);
+          dp[1] = make_uint4(fx.qb[j], 0, 0, 0);
         }
       }
-    }
-  }
-  // queues back to the rings, heads at slot 0 (a message in flight at the launch's end: rare)
-  if (__builtin_amdgcn_ballot_w64(wb && (qmask || rmask))) {            // wave-uniform
+      uint4* rp = reinterpret_cast<uint4*>(qslots(S, c * N + fx.L, 1));
+      uint32_t n = 0;
 #pragma unroll
-    for (int j = 0; j < F; ++j) {
-      if (wb && ((qmask >> j) & 1)) {
-        uint4* dp = reinterpret_cast<uint4*>(qslots(S, c * N + fk(j), 0));
-        dp[0] = make_uint4(qA[j], RAFT_MSG_APPEND_ENTRIES | Lid << 3, qT[j], qa[j]);
-        dp[1] = make_uint4(qb[j], 0, 0, 0);
+      for (int j = 0; j < F; ++j) {
+        if (active && ((fx.rmask >> j) & 1)) {
+          uint4* dp = rp + 2 * n;
+          dp[0] = make_uint4(fx.resA, RAFT_MSG_APPEND_RESPONSE | (fx.fk(j) + 1) << 3 | fx.rH[j] << 7,
+                             fx.rT[j], fx.rA[j]);
+          dp[1] = make_uint4(fx.rB[j], 0, 0, 0);
+          ++n;
+        }
       }
     }
-    uint4* rp = reinterpret_cast<uint4*>(qslots(S, c * N + L, 1));
-    uint32_t n = 0;
+#ifdef RS_WAVELOG
+    wl_loop = wl_x1 = wl_x2 = wl_x3 = wl_lend = wall_clock64();
+#endif
+  } else {
+#ifdef RS_WAVELOG
+    wl_loop = wall_clock64();
+#endif
+    auto field = [&](int f, uint32_t (&out)[N]) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) out[k] = w[HOT_CW + f * N + k];
+    };
+    uint32_t nfl[N], nqm[N];
+    field(HF_FLAGS, nfl);
+    field(HF_QMETA, nqm);
+    // exactly one leader; every node running; only the leader has leader-state
+    uint32_t L = 0, nlead = 0, badn = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const uint32_t f = nfl[k];
+      const bool lead = (f & 3) == RAFT_LEADER;
+      L = lead ? (uint32_t)k : L;
+      nlead += lead;
+      badn |= ((f >> 10) & 7) | (lead != (((f >> 14) & 1) != 0)) | (lead && (f & FL_DRAW));
+    }
+    bool bad = !active || nlead != 1 || badn != 0 || S.Q < (uint32_t)F;
+    const uint32_t Lid = L + 1;
+    // follower slot j is node j (j < L) or j + 1 (j >= L)
+    auto fsel = [&](const uint32_t (&v)[N], int j) { return msel((uint32_t)j >= L, v[j + 1], v[j]); };
+    auto fk = [&](int j) { return (uint32_t)j + ((uint32_t)j >= L ? 1u : 0u); };
+
+    uint32_t tmp[N];
+    // leader registers
+    const uint32_t Lfl = pick<N>(nfl, L);
+    field(HF_MASKS, tmp); uint32_t Lmk = pick<N>(tmp, L);
+    uint32_t fmk[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) fmk[j] = fsel(tmp, j);
+    field(HF_TERM, tmp); const uint32_t Lterm = pick<N>(tmp, L);
+    uint32_t fterm[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) fterm[j] = fsel(tmp, j);
+    field(HF_COMMIT, tmp); const uint32_t Lcommit = pick<N>(tmp, L);
+    uint32_t fcommit[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) fcommit[j] = fsel(tmp, j);
+    field(HF_LEN, tmp); const uint32_t Llen = pick<N>(tmp, L);
+    uint32_t flen[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) flen[j] = fsel(tmp, j);
+    field(HF_DEADLINE, tmp); uint32_t Ldl = pick<N>(tmp, L);
+    uint32_t fdl[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) fdl[j] = fsel(tmp, j);
+    uint32_t tlo[N], thi[N];
+    field(HF_TRACE_LO, tlo);
+    field(HF_TRACE_HI, thi);
+    uint64_t Ltr = (uint64_t)pick<N>(thi, L) << 32 | pick<N>(tlo, L);
+    uint64_t ftr[F];
+    uint32_t ffl[F];
 #pragma unroll
     for (int j = 0; j < F; ++j) {
-      if (wb && ((rmask >> j) & 1)) {
-        const uint32_t sid = fk(j) + 1;
-        uint4* dp = rp + 2 * n;
-        dp[0] = make_uint4(resA, RAFT_MSG_APPEND_RESPONSE | sid << 3 | rH[j] << 7, rT[j], rA[j]);
-        dp[1] = make_uint4(rB[j], 0, 0, 0);
-        ++n;
+      ftr[j] = (uint64_t)fsel(thi, j) << 32 | fsel(tlo, j);
+      ffl[j] = fsel(nfl, j);
+    }
+    // the leader's rows for its followers: next_index / match_index of peer id fk(j) + 1
+    int32_t nx[F], mt[F];
+    {
+      uint32_t rn[N], rm[N];                    // the leader's next / match of each peer id p + 1
+#pragma unroll
+      for (int p = 0; p < N; ++p) {
+        field(HF_NEXT + p, tmp);
+        rn[p] = pick<N>(tmp, L);
+        field(HF_NEXT + N + p, tmp);
+        rm[p] = pick<N>(tmp, L);
+      }
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        nx[j] = (int32_t)fsel(rn, j);
+        mt[j] = (int32_t)fsel(rm, j);
       }
     }
-  }
+    int32_t nx0[F], mt0[F];                     // as loaded: unchanged words are not stored back
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      nx0[j] = nx[j];
+      mt0[j] = mt[j];
+    }
+    const bool ackbad = Llen > w[CLW];          // a success response would be checker work (P4)
+    const uint32_t Lkeys = Lmk >> 16;
+    // heartbeats need full leader-state, no LazySeq log and commit within the log
+    // (append-entries-rpc's IOOBE/NPE/CCE checks, core.clj:56-67): constant over the launch
+    bad = bad || (Lkeys & (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid))) !=
+                     (((1u << (N + 1)) - 1) & ~1u & ~(1u << Lid)) ||
+          ((Lfl >> 13) & 1) || Lcommit > Llen;
+
+#ifdef RS_WAVELOG
+    asm volatile("" ::"v"(Ltr), "v"(fdl[0]), "v"(nx[0]));
+    wl_x1 = wall_clock64();                     // fields extracted
+#endif
+    // ---------------------------------------------------------------- queued messages
+    uint32_t qmask = 0, rmask = 0, resA = INF;
+    uint32_t qA[F], qT[F], qa[F], qb[F], rT[F], rA[F], rB[F], rH[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      qA[j] = INF; qT[j] = qa[j] = qb[j] = 0;
+      rT[j] = rA[j] = rB[j] = rH[j] = 0;
+    }
+    if (!bad) {
+      const uint32_t Lqm = pick<N>(nqm, L);
+      bad = (Lqm >> 4) & 31;                                   // the leader's REQ queue is empty
+      const uint32_t rsh = (Lqm >> 9) & 15, rsc = (Lqm >> 13) & 31;
+      uint32_t need = 0, rqh[F];
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const uint32_t qm = fsel(nqm, j);
+        const uint32_t rqc = (qm >> 4) & 31;
+        rqh[j] = qm & 15;
+        bad = bad || rqc > 1 || ((qm >> 13) & 31) != 0;       // <= 1 request, no responses
+        need |= (uint32_t)(rqc != 0) << j;
+      }
+      bad = bad || rsc > (uint32_t)F;
+      // The messages: loaded by every lane of a wave in which any lane has one (a message in flight
+      // at the launch's start is rare), all loads issued before any is looked at -- one memory round
+      // trip, where loads under per-lane branches each waited for the last. Slot indices are
+      // clamped into the ring for lanes whose queue words are not looked at.
+      uint4 qm0[F], qm1[F], rm0[F], rm1[F];
+      if (__builtin_amdgcn_ballot_w64(!bad && (need || rsc))) {     // wave-uniform
+#pragma unroll
+        for (int j = 0; j < F; ++j) {                          // the leader's append-entries
+          const uint4* mp = reinterpret_cast<const uint4*>(
+              qslots(S, c * N + fk(j), 0) + min(rqh[j], S.Q - 1) * qstride(S, 0));
+          qm0[j] = mp[0];
+          qm1[j] = mp[1];
+        }
+#pragma unroll
+        for (int i = 0; i < F; ++i) {                          // append-responses, sender order
+          const uint4* mp = reinterpret_cast<const uint4*>(
+              qslots(S, c * N + L, 1) + min(wrapq(rsh + i, S.Q), S.Q - 1) * qstride(S, 1));
+          rm0[i] = mp[0];
+          rm1[i] = mp[1];
+        }
+      }
+      if (!bad) {
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          if ((need >> j) & 1) {
+            const uint4 m0 = qm0[j], m1 = qm1[j];
+            bad = bad || m0.y != (RAFT_MSG_APPEND_ENTRIES | Lid << 3) || m1.y || m1.z || m1.w;
+            qmask |= 1u << j;
+            qA[j] = m0.x; qT[j] = m0.z; qa[j] = m0.w; qb[j] = m1.x;
+          }
+        }
+        uint32_t last = 0;
+#pragma unroll
+        for (int i = 0; i < F; ++i) {
+          if ((uint32_t)i < rsc && !bad) {
+            const uint4 m0 = rm0[i], m1 = rm1[i];
+            const uint32_t hdr = m0.y, src = (hdr >> 3) & 15;
+            bad = (hdr & 7) != RAFT_MSG_APPEND_RESPONSE || (hdr >> 8) || m1.y || m1.z || m1.w ||
+                  src <= last || src > (uint32_t)N || src == Lid || (i && m0.x != resA);
+            last = src;
+            resA = m0.x;
+            const uint32_t j = src - 1 - (src > Lid ? 1u : 0u);
+            if (!bad) {
+              rmask |= 1u << j;
+#pragma unroll
+              for (int jj = 0; jj < F; ++jj) {
+                if ((uint32_t)jj == j) {
+                  rT[jj] = m0.z; rA[jj] = m0.w; rB[jj] = m1.x; rH[jj] = (hdr >> 7) & 1;
+                }
+              }
+            }
+          }
+        }
+      }
+      if (!rmask) resA = INF;
+    }
+    record_bail(active && bad, t0);           // outside the model from the start: bail at t0
+    wb = active && !bad;
+    bool run = wb;
+
+    // ---------------------------------------------------------------- the cluster's ticks
+    uint32_t tn = t0;
+    // followers whose deadline holds its lower bound t_ae + el_base (the draw is deferred)
+    // (a draw owed from an earlier launch: FL_DRAW in the follower's flags, device.hpp)
+    uint32_t fpend = 0;
+#pragma unroll
+    for (int j = 0; j < F; ++j) fpend |= ((ffl[j] & FL_DRAW) ? 1u : 0u) << j;
+    auto draw_deadlines = [&](uint32_t due) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if ((due >> j) & 1) {
+          const uint4 wd = event_draw(g, fk(j) + 1, fdl[j] - S.el_base, S);   // D4, core.clj:174
+          fdl[j] += __umulhi(wd.y, S.el_span);
+        }
+      }
+      fpend &= ~due;
+    };
+    auto next_event = [&]() {
+      uint32_t m = min(Ldl, resA);
+#pragma unroll
+      for (int j = 0; j < F; ++j) m = min(m, min(fdl[j], qA[j]));
+      return m;
+    };
+    // The cluster at its fixed point: every follower took the leader's append-entries (flags,
+    // votes, term and commit are what another one sets again), every response succeeded (next /
+    // match / keys as another one sets them), the log is empty (a heartbeat ships nothing) and no
+    // message is in flight. If the followers' re-armed timers (>= t_ae + el_base) cannot fire
+    // before the next round's append-entries (el_base >= the round period P) and the leader's
+    // responses all fit before its next heartbeat (hb >= 2d + F), every later round is this one
+    // shifted by a multiple of P: only the ticks in the trace hashes change.
+    auto at_fixed_point_state = [&]() {
+      bool ok = Llen == 0 && !ackbad;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        ok = ok && fterm[j] == Lterm &&
+             (ffl[j] & (3u | 15u << 2 | 15u << 6 | 1u << 13)) == (RAFT_FOLLWER | Lid << 6) &&
+             fcommit[j] == flen[j] && (fmk[j] & 0xFFFFu) == 0 && nx[j] == 0 &&
+             mt[j] == (int32_t)Lcommit;
+      return ok;
+    };
+    auto at_fixed_point = [&]() {
+      return S.el_base >= P && S.hb >= 2 * d + F && !qmask && !rmask && at_fixed_point_state();
+    };
+    // From the fixed point with the next heartbeat at th, every round to the launch's end as trace
+    // hashes: the rounds that end before it, then the one it cuts (heartbeat, append-entries and
+    // responses up to tend - 1; what is left is queued as the general body leaves it): every next
+    // event of the cluster is then at or after tend.
+    auto fixed_point_rounds = [&](uint32_t th) {   // FixedPoint::rounds on this path's registers
+      FixedPoint<N> x;
+      x.L = L; x.Lid = Lid; x.Lterm = Lterm; x.Lcommit = Lcommit;
+      x.Ltr = Ltr; x.Ldl = Ldl; x.fpend = fpend; x.qmask = qmask; x.rmask = rmask; x.resA = resA;
+      x.nhb = nhb; x.nae = nae; x.nar = nar;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        x.ftr[j] = ftr[j]; x.fdl[j] = fdl[j];
+        x.qA[j] = qA[j]; x.qT[j] = qT[j]; x.qa[j] = qa[j]; x.qb[j] = qb[j];
+        x.rT[j] = rT[j]; x.rA[j] = rA[j]; x.rB[j] = rB[j]; x.rH[j] = rH[j];
+      }
+      x.rounds(th, tend, d, S.hb, S.el_base);
+      Ltr = x.Ltr; Ldl = x.Ldl; fpend = x.fpend; qmask = x.qmask; rmask = x.rmask; resA = x.resA;
+      nhb = x.nhb; nae = x.nae; nar = x.nar;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        ftr[j] = x.ftr[j]; fdl[j] = x.fdl[j];
+        qA[j] = x.qA[j]; qT[j] = x.qT[j]; qa[j] = x.qa[j]; qb[j] = x.qb[j];
+        rT[j] = x.rT[j]; rA[j] = x.rA[j]; rB[j] = x.rB[j]; rH[j] = x.rH[j];
+      }
+    };
+
+    // ------------------------------------------- the fixed-point path (C2's steady state)
+    // A cluster at its fixed point (above) whose round in progress at t0 is on the period-P
+    // schedule -- none (the next heartbeat at Ldl >= t0), its append-entries in flight, or its
+    // responses pending exactly as the last launch's end cut them -- and whose followers' timers
+    // cannot fire before their next append-entries runs every event of the launch here: the rest
+    // of that round event by event, then fixed_point_rounds. Everything else is the general loop's.
+    bool fp = wb && S.el_base >= P && S.hb >= 2 * d + F && (vouched || at_fixed_point_state());
+    uint32_t th0 = Ldl, mid = 0;               // the round's heartbeat; 1 AEs in flight, 2 responses
+    if (qmask) {
+      mid = 1;
+      th0 = qA[0] - d;
+      fp = fp && qmask == allF && !rmask && qA[0] >= t0 && qA[0] >= d && Ldl == th0 + S.hb;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        fp = fp && qA[j] == qA[0] && qT[j] == Lterm && qa[j] == Lcommit && qb[j] == 0;
+    } else if (rmask) {
+      mid = 2;
+      th0 = resA - 2 * d;
+      const uint32_t j0 = (uint32_t)F - __popc(rmask);          // responses already taken
+      const int64_t cut = (int64_t)t0 - ((int64_t)th0 + 2 * d);  // what the last launch's end cut
+      fp = fp && resA >= 2 * d && rmask == (allF & ~((1u << j0) - 1)) &&
+           (int64_t)j0 == (cut < 0 ? 0 : cut > F ? (int64_t)F : cut) &&
+           Ldl == (j0 ? th0 + 2 * d + j0 - 1 : th0) + S.hb;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        fp = fp && (!((rmask >> j) & 1) ||
+                    (rT[j] == Lterm && rA[j] == Lcommit && rB[j] == 0 && rH[j] == 1));
+    } else {
+      fp = fp && Ldl >= t0;
+    }
+    {
+      const uint32_t nxt = min((mid == 2 ? th0 + P : th0) + d, tend);   // the next AE (or the end)
+#pragma unroll
+      for (int j = 0; j < F; ++j) fp = fp && fdl[j] >= nxt;
+    }
+    // A vouched cluster off the fixed-point path (set_tick moved the clock, ...) has no full state
+    // here: the general body runs it from t0.
+    const bool vbail = vouched && wb && !fp;
+    record_bail(vbail, t0);
+    if (vbail) wb = run = false;
+#ifdef RS_WAVELOG
+    asm volatile("" ::"v"(fp), "v"(th0));
+    wl_x2 = wall_clock64();                     // queued messages read, fixed-point path decided
+#endif
+    if (fp) {
+      run = false;
+      bool whole = true;                        // the round in progress finished in this launch
+      if (mid == 1) {
+        const uint32_t ta = qA[0];
+        if (ta < tend) {                        // the append-entries
+#pragma unroll
+          for (int j = 0; j < F; ++j) {
+            ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, Lterm, RAFT_FOLLWER,
+                                 Lterm, 0);
+            fdl[j] = ta + S.el_base;
+            qA[j] = INF;
+            rT[j] = Lterm; rA[j] = Lcommit; rB[j] = 0; rH[j] = 1;
+          }
+          fpend = allF;
+          qmask = 0;
+          rmask = allF;
+          resA = ta + d;
+          nae += F;
+        } else {
+          whole = false;
+        }
+      }
+      if (mid && whole) {                       // the responses, one per tick in slot order
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const uint32_t tau = th0 + 2 * d + j;
+          if (((rmask >> j) & 1) && tau < tend) {
+            Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, fk(j) + 1, Lterm, RAFT_LEADER,
+                              Lterm, 0);
+            rmask &= ~(1u << j);
+            Ldl = tau + S.hb;
+            ++nar;
+          }
+        }
+        if (rmask) whole = false;
+        else resA = INF;
+      }
+      if (whole) fixed_point_rounds(mid ? th0 + P : th0);
+    }
+#ifdef RS_WAVELOG
+    asm volatile("" ::"v"(Ltr), "v"(ftr[0]), "v"(Ldl));
+    wl_x3 = wall_clock64();                     // the fixed-point path's rounds done
+#endif
+#ifdef RS_WAVELOG
+    wl_ts = __builtin_amdgcn_s_memtime();
+#endif
+    bool pbail = false;                        // bailed in the last trip, not yet recorded
+    uint32_t pbt = 0;
+    for (;;) {
+      record_bail(pbail, pbt);                 // the loop's head: every lane active
+      pbail = false;
+      uint32_t t = max(tn, next_event());
+      // a deferred deadline at or before the tick to decide is drawn first (it can only move later)
+      for (;;) {
+        uint32_t due = 0;
+#pragma unroll
+        for (int j = 0; j < F; ++j) due |= (uint32_t)(fdl[j] <= t) << j;
+        due &= fpend;
+        if (!run || t >= tend || !due) break;
+        draw_deadlines(due);
+        t = max(tn, next_event());
+      }
+      const bool on = run && t < tend;
+      if (!__builtin_amdgcn_ballot_w64(on)) break;
+#ifdef RS_WAVELOG
+      if (!wl_trips) wl_first = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(on));
+      ++wl_trips;
+#endif
+      RS_LPH(0);
+      if (!on) continue;
+      // ------------------------------------------------ decide on the pre-tick state
+      const bool lres = rmask != 0 && resA <= t;               // a message beats the deadline
+      const bool lhb = !lres && Ldl <= t;
+      uint32_t fae = 0, fto = 0;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const bool a = qA[j] <= t;
+        fae |= (uint32_t)a << j;
+        fto |= (uint32_t)(!a && fdl[j] <= t) << j;
+      }
+      bool bail = fto != 0;                                    // a follower's election timeout
+      if (lhb) {
+        bail = bail || qmask != 0;                             // a follower still holds one
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const uint32_t pv = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
+          bail = bail || pv < Llen || pv >= (1u << 24);        // entries to ship
+        }
+      }
+      const int hs = __builtin_ctz(rmask | (1u << F));
+      uint32_t xT = 0, xH = 0;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if (j == hs) {
+          xT = rT[j]; xH = rH[j];
+        }
+      }
+      const uint32_t xid = (uint32_t)hs + 1 + ((uint32_t)hs >= L ? 1u : 0u);
+      if (lres)
+        bail = bail || xT > Lterm || (xH ? ackbad : ((Lmk >> (16 + xid)) & 1) == 0);
+      if (fae) {
+        bail = bail || rmask != 0;                             // responses of two ticks
+#pragma unroll
+        for (int j = 0; j < F; ++j)
+          if ((fae >> j) & 1)
+            bail = bail || qb[j] != 0 || !(qT[j] < fterm[j] || flen[j] <= fcommit[j]);
+      }
+      RS_LPH(1);
+      if (bail) {                              // the general tick body runs this tick
+        pbail = true;
+        pbt = t;
+        run = false;
+        continue;
+      }
+      // ------------------------------------------------ run
+      uint32_t tl = t;                         // the last tick run (a round or a drain runs more)
+      bool round = false;
+      if (lhb) {                               // heartbeat-handler: empty append-entries to all
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          qA[j] = t + d; qT[j] = Lterm; qa[j] = Lcommit;
+          qb[j] = nx[j] - 1 > 0 ? (uint32_t)(nx[j] - 1) : 0u;
+        }
+        qmask = (1u << F) - 1;
+        Ldl = t + S.hb;
+        Ltr = trace_event(Ltr, t, 7, 0, 0, RAFT_LEADER, Lterm, 0);
+        ++nhb;
+        // The whole heartbeat round in this trip when nothing else can happen before its last
+        // response: every follower takes the append-entries at t + d (no follower deadline before
+        // it; the handler's checks pass), the followers' re-armed deadlines (>= t + d + el_base) and
+        // the leader's (t + hb) fall after the responses at t + 2d .. t + 2d + F - 1, and the
+        // append-entries come before the launch ends (and no older response is still queued). The
+        // responses then run in slot order up to the launch end (the rest stay queued) and stop at
+        // one outside the model (the next trip decides it). A deferred deadline counts with its
+        // lower bound here (a round not taken is run tick by tick).
+        round = rmask == 0 && S.hb >= 2 * d + F && S.el_base >= d + F && tend - t > d;
+#pragma unroll
+        for (int j = 0; j < F; ++j)
+          round = round && fdl[j] >= t + d && qb[j] == 0 && (Lterm < fterm[j] || flen[j] <= fcommit[j]);
+      }
+      RS_LPH(2);
+      // A trip runs exactly one of: a whole round (below), a heartbeat alone (its round did not fit:
+      // the append-entries are taken one tick later as `fae`), append-entries that arrived (fae),
+      // or queued responses (lres): a heartbeat with a follower still holding an append-entries,
+      // and append-entries with responses still queued, were bailed above.
+      auto append_entries = [&](uint32_t ta, uint32_t fa) {   // append-entries-handler, followers fa
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          if ((fa >> j) & 1) {
+            const uint32_t mterm = qT[j], rterm = fterm[j];
+            const bool ok = mterm >= fterm[j];
+            const uint32_t nfl2 = ok ? (ffl[j] & ~(3u | 15u << 2 | 15u << 6 | 1u << 13)) |
+                                           RAFT_FOLLWER | Lid << 6
+                                     : ffl[j];
+            const uint32_t nterm = ok ? mterm : fterm[j];
+            ftr[j] = trace_event(ftr[j], ta, RAFT_MSG_APPEND_ENTRIES, Lid, mterm, nfl2 & 3, nterm, 0);
+            if (ok) {
+              fcommit[j] = flen[j];                            // apply-entries! (nothing applied)
+              fmk[j] &= 0xFFFF0000u;
+            }
+            fterm[j] = nterm;
+            ffl[j] = nfl2;
+            // the response: to the leader's RES queue, in sender id order
+            rT[j] = rterm; rA[j] = ok ? qa[j] : 0u; rB[j] = 0; rH[j] = ok;
+            qA[j] = INF;
+            fdl[j] = ta + S.el_base;                           // + the deferred draw
+          }
+        }
+        fpend |= fa;
+        qmask &= ~fa;
+        rmask = fa;
+        resA = ta + d;
+        nae += __popc(fa);
+        tl = ta;
+      };
+      // append-response-handler for follower slot j's response at tick tau (core.clj:141-149);
+      // false (and nothing done) when it is outside the model: a newer term, a success response
+      // that would be checker work, or a failure without the peer's key (NPE)
+      auto response = [&](int j, uint32_t tau, uint32_t yT, uint32_t yA, uint32_t yB, uint32_t yH,
+                          int32_t& nxj, int32_t& mtj) {
+        const uint32_t yid = fk(j) + 1;
+        if (yT > Lterm || (yH ? ackbad : ((Lmk >> (16 + yid)) & 1) == 0)) return false;
+        rmask &= ~(1u << j);
+        Lmk |= yH << (16 + yid);
+        nxj = yH ? (int32_t)yB : nxj - 1;
+        mtj = yH ? (int32_t)yA : mtj;
+        Ldl = tau + S.hb;
+        Ltr = trace_event(Ltr, tau, RAFT_MSG_APPEND_RESPONSE, yid, yT, RAFT_LEADER, Lterm, 0);
+        ++nar;
+        tl = tau;
+        return true;
+      };
+      if (round) {
+        // every follower at t + d, then the responses at t + 2d .. t + 2d + F - 1 in slot order (the
+        // round's conditions put them all before the launch end and every follower's next event):
+        // straight-line code, every index static
+        append_entries(t + d, (1u << F) - 1);
+        bool go = true;
+#pragma unroll
+        for (int j = 0; j < F; ++j)     // (a round cut by the launch end leaves the rest queued)
+          go = go && t + 2 * d + j < tend &&
+               response(j, t + 2 * d + j, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
+        if (!rmask) resA = INF;
+        if (at_fixed_point()) {
+          fixed_point_rounds(t + P);
+          tl = tend - 1;                       // nothing of the cluster is left before tend
+        }
+      } else if (fae || lres) {
+        // fae: the append-entries at t, then their responses from t + d in the same trip unless
+        // the leader's heartbeat falls due before them. The responses run one per tick, heads in
+        // sender order, while nothing else in the cluster is due (the followers' next events and
+        // the launch end; the leader's own deadline moves past each); lres: the first one at t
+        // was decided above. A response outside the model ends the run and the next trip
+        // decides it. A round finished here (one the last launch cut) continues at the fixed point.
+        uint32_t tau0 = t;
+        if (fae) {
+          append_entries(t, fae);
+          tau0 = Ldl >= t + d ? t + d : tend;
+        }
+        uint32_t E = tend;
+#pragma unroll
+        for (int j = 0; j < F; ++j) E = min(E, min(fdl[j], qA[j]));
+        if (lres) E = max(E, t + 1);
+        for (uint32_t tau = tau0; rmask && tau < E; ++tau) {
+          const int h2 = __builtin_ctz(rmask);
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < F; ++j)
+            if (j == h2) ok = response(j, tau, rT[j], rA[j], rB[j], rH[j], nx[j], mt[j]);
+          if (!ok) break;
+          if (!rmask) resA = INF;
+        }
+        if (at_fixed_point() && Ldl > tl) {
+          fixed_point_rounds(Ldl);
+          tl = tend - 1;
+        }
+      }
+      RS_LPH(4);
+      tn = tl + 1;
+    }
+    // the draws still owed stay owed in the stored state (FL_DRAW): a cluster at its fixed point
+    // makes none at all
+
+#ifdef RS_WAVELOG
+    wl_lend = wall_clock64();
+#endif
+    // ---------------------------------------------------------------- write back
+    if (S.shist) {
+      // packing key for the next launch (bailed clusters get theirs from the catch-up below); the
+      // wave's clusters share a few keys: one histogram atomic per distinct key
+      const bool kl = wb && run;
+      const uint32_t key = kl ? sched_bucket(next_event(), tend) : INF;
+      if (kl) S.skey[c] = key;
+      uint64_t pend = __builtin_amdgcn_ballot_w64(kl);
+      while (pend) {
+        const uint32_t k = (uint32_t)__shfl((int)key, (int)__builtin_ctzll(pend));
+        const uint64_t same = __builtin_amdgcn_ballot_w64(kl && key == k);
+        if (lane == (uint32_t)__builtin_ctzll(pend)) atomicAdd(&S.shist[k], (uint32_t)__popcll(same));
+        pend &= ~same;
+      }
+    }
+    const bool wfp = !__builtin_amdgcn_ballot_w64(wb && !fp);
+    if (wb) {
+      // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
+      constexpr int NV = HF_NEXT;
+      uint32_t v[NV][N];
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        // node k is the leader (k == L) or follower slot k - 1 (k > L) / k (k < L)
+        const bool isL = (uint32_t)k == L;
+        const int jl = k > 0 ? k - 1 : 0, jh = k < F ? k : F - 1;
+        const bool lo = (uint32_t)k > L;
+        auto fv = [&](const uint32_t* x) { return msel(lo, x[jl], x[jh]); };
+        const uint32_t fq = (qmask >> (lo ? jl : jh)) & 1;
+        const uint32_t fqa = fv(qA);
+        const uint64_t trf = (uint64_t)msel(lo, (uint32_t)(ftr[jl] >> 32), (uint32_t)(ftr[jh] >> 32)) << 32 |
+                            msel(lo, (uint32_t)ftr[jl], (uint32_t)ftr[jh]);
+        const uint64_t tr = isL ? Ltr : trf;
+        v[HF_FLAGS][k] = isL ? Lfl : (fv(ffl) & ~FL_DRAW) | (((fpend >> (lo ? jl : jh)) & 1) ? FL_DRAW : 0u);
+        v[HF_MASKS][k] = isL ? Lmk : fv(fmk);
+        v[HF_TERM][k] = isL ? Lterm : fv(fterm);
+        v[HF_COMMIT][k] = isL ? Lcommit : fv(fcommit);
+        v[HF_LEN][k] = isL ? Llen : fv(flen);
+        v[HF_DEADLINE][k] = isL ? Ldl : fv(fdl);
+        v[HF_QMETA][k] = isL ? pack_qmeta(0, 0, 0, __popc(rmask)) : pack_qmeta(0, fq, 0, 0);
+        v[HF_REQ_ARR][k] = isL ? INF : (fq ? fqa : INF);
+        v[HF_RES_ARR][k] = isL ? resA : INF;
+        v[HF_REQ_TAIL][k] = isL ? 0u : (fq ? fqa : 0u);
+        v[HF_RES_TAIL][k] = isL ? (rmask ? resA : 0u) : 0u;
+        v[HF_TRACE_LO][k] = (uint32_t)tr;
+        v[HF_TRACE_HI][k] = (uint32_t)(tr >> 32);
+      }
+      auto live = [](int q) { return q >= (int)HOT_CW && q < (int)(HOT_CW + HF_NEXT * N); };
+      auto val = [&](int q) { return v[(q - HOT_CW) / N][(q - HOT_CW) % N]; };
+      // The changed chunks into the image (in a heartbeat round the deadlines and trace hashes
+      // change, all in the block's first line; flags, terms, masks, commits, queue words and rows
+      // come back unchanged); the lines they dirty go back to memory whole, below.
+      // A wave whose written-back clusters all took the fixed-point path changed nothing past the
+      // queue words and the flags' FL_DRAW (masks, terms, commits, lengths and rows are the fixed
+      // point's).
+      const int ch_end = wfp ? (int)(HOT_CW + (HF_FLAGS + 1) * N + 3) / 4
+                             : (int)(HOT_CW + HF_NEXT * N + 3) / 4;
+      // (every chunk is written back to the image, changed or not: no branch per chunk)
+#pragma unroll
+      for (int i = (int)HOT_CW / 4; i < (int)(HOT_CW + HF_NEXT * N + 3) / 4; ++i) {
+        if (i < ch_end) {                                    // wave-uniform
+          const int q = 4 * i;
+          const uint4 x = make_uint4(live(q) ? val(q) : w[q], live(q + 1) ? val(q + 1) : w[q + 1],
+                                     live(q + 2) ? val(q + 2) : w[q + 2],
+                                     live(q + 3) ? val(q + 3) : w[q + 3]);
+          *lds_at<uint4>(img, img_off(lane, i)) = x;
+          dl |= (uint32_t)(x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3])
+                << (i / 8);
+        }
+      }
+      // the steady certificate for the next launch: the cluster stays at its fixed point
+      const uint32_t cn = fp || (full && at_fixed_point_state()) ? (CERT_MAGIC | L) : 0u;
+      *lds_at<uint4>(img, img_off(lane, CL_CERT / 4)) = make_uint4(w[4], w[5], w[6], cn);
+      dl |= (uint32_t)(cn != w[CL_CERT]);
+      // the leader's rows (node L): next / match of peer fk(j) + 1
+      if (!wfp) {
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const uint32_t qn = HOT_CW + (HF_NEXT + fk(j)) * N + L;
+          const uint32_t qt = HOT_CW + (HF_NEXT + N + fk(j)) * N + L;
+          if (nx[j] != nx0[j]) {
+            *lds_at<uint32_t>(img, img_off(lane, qn / 4) + 4 * (qn % 4)) = (uint32_t)nx[j];
+            dl |= 1u << (qn / 32);
+          }
+          if (mt[j] != mt0[j]) {
+            *lds_at<uint32_t>(img, img_off(lane, qt / 4) + 4 * (qt % 4)) = (uint32_t)mt[j];
+            dl |= 1u << (qt / 32);
+          }
+        }
+      }
+    }
+    // queues back to the rings, heads at slot 0 (a message in flight at the launch's end: rare)
+    if (__builtin_amdgcn_ballot_w64(wb && (qmask || rmask))) {            // wave-uniform
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if (wb && ((qmask >> j) & 1)) {
+          uint4* dp = reinterpret_cast<uint4*>(qslots(S, c * N + fk(j), 0));
+          dp[0] = make_uint4(qA[j], RAFT_MSG_APPEND_ENTRIES | Lid << 3, qT[j], qa[j]);
+          dp[1] = make_uint4(qb[j], 0, 0, 0);
+        }
+      }
+      uint4* rp = reinterpret_cast<uint4*>(qslots(S, c * N + L, 1));
+      uint32_t n = 0;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if (wb && ((rmask >> j) & 1)) {
+          const uint32_t sid = fk(j) + 1;
+          uint4* dp = rp + 2 * n;
+          dp[0] = make_uint4(resA, RAFT_MSG_APPEND_RESPONSE | sid << 3 | rH[j] << 7, rT[j], rA[j]);
+          dp[1] = make_uint4(rB[j], 0, 0, 0);
+          ++n;
+        }
+      }
+    }
+  }   // the general path
   // Dirty lines back to memory whole: a wave instruction writes eight clusters' line (8 lanes x
   // 16 B each), read from the image (line ln of cluster cc is its chunks 8 ln .. 8 ln + 7): the
   // eight reads of a line first, then the stores. The stores write through to memory (sc1: the
@@ -937,6 +1159,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #ifdef RS_WAVELOG
   {
     const uint64_t wl_end = wall_clock64();
+    const uint32_t wl_events = nhb + nae + nar;
     const uint32_t emax = ~wave_min(~wl_events), emin = wave_min(wl_events);
     if (lane == 0 && S.wavelog) {
       uint32_t hw, xcc;
@@ -949,6 +1172,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       rec[2] = make_uint4((uint32_t)(wl_loop - wl_start), (uint32_t)(wl_lend - wl_start), emin, emax);
       rec[3] = make_uint4(wl_ph[0], wl_ph[1], wl_ph[2], wl_ph[3]);
       rec[4] = make_uint4(wl_ph[4], 0, 0, 0);
+      rec[5] = make_uint4((uint32_t)(wl_x1 - wl_start), (uint32_t)(wl_x2 - wl_start),
+                          (uint32_t)(wl_x3 - wl_start), 0);
     }
   }
 #endif

@@ -33,6 +33,12 @@ print("load us     p0/10/50/90/99/100:", q(a[:, 8] / 100.0))
 print("loop us     p0/10/50/90/99/100:", q((a[:, 9] - a[:, 8]) / 100.0))
 print("wb us       p0/10/50/90/99/100:", q((end - start - a[:, 9]) / 100.0))
 print("trips       p0/10/50/90/99/100:", q(a[:, 4]))
+if (a[:, 20] | a[:, 21] | a[:, 22]).any():   # fixed-point path stamps (round-5 builds)
+    x1, x2, x3 = a[:, 20], a[:, 21], a[:, 22]
+    print("  load..extracted  us:", q((x1 - a[:, 8]) / 100.0))
+    print("  ..fp decided     us:", q((x2 - x1) / 100.0))
+    print("  ..fp rounds done us:", q((x3 - x2) / 100.0))
+    print("  ..general loop   us:", q((a[:, 9] - x3) / 100.0))
 print("lanes on    p0/10/50/90/99/100:", q(a[:, 7]))
 print("events/lane min p0/10/50/90/99/100:", q(a[:, 10]))
 print("events/lane max p0/10/50/90/99/100:", q(a[:, 11]))
