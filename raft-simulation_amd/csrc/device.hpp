@@ -225,13 +225,17 @@ __device__ inline uint32_t on_tick(uint64_t j, uint32_t P, const DivU32& B) {
   const uint64_t t = P ? (uint64_t)q * P + (j32 - q * B.d) : j32;
   return t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
 }
+// The on-tick number of on-tick t (the inverse of on_tick).
+__device__ __forceinline__ uint64_t on_index(uint32_t t, const DevSim& S) {
+  const uint32_t P = S.client_period;
+  const uint32_t q = P ? udiv(S.div_period, t) : 0u;
+  return P ? (uint64_t)q * S.div_burst.d + (t - q * P) : t;
+}
 // The next injection after the one at tick t (an on-tick), drawing gap word w.
 __device__ inline uint32_t client_next_tick(uint32_t t, uint32_t w, const DevSim& S,
                                             const uint32_t* pw) {
-  const uint32_t P = S.client_period;
-  const uint32_t q = P ? udiv(S.div_period, t) : 0u;
-  const uint64_t j = P ? (uint64_t)q * S.div_burst.d + (t - q * P) : t;
-  return on_tick(j + 1 + client_gap(w, pw, S.client_top), P, S.div_burst);
+  return on_tick(on_index(t, S) + 1 + client_gap(w, pw, S.client_top), S.client_period,
+                 S.div_burst);
 }
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
   return (h ^ w) * 0x100000001B3ull;

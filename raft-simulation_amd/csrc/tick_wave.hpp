@@ -515,19 +515,50 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // own) runs their injections up to the launch's end here, one Philox draw each, with no trip;
     // its trip loop then finds no event before tend. A wave that mixes live clusters in takes the
     // trips (draining a dead cluster's injections there would stall its live wave mates).
-    if constexpr (!LITE && !SPEC) {
+    // Injections into a dead cluster are independent draws (keyed by the injection count), so the
+    // wave runs them 64 at a time, one cluster after another: lane l draws the gap after the
+    // cluster's (count + l)-th injection, an inclusive scan of (1 + gap) over the lanes gives the
+    // next 64 injections' on-tick numbers, and the first one at or past tend ends the cluster's
+    // run (SIM_SPEC P0; the Spec-Raft control's client-sets reach halted nodes the same way).
+    if constexpr (!LITE) {
       const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
       if (S.client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
-        uint32_t cnt = 0;
-        while (active && cnext < tend) {
-          const uint4 d = philox(g, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
-          ++cnt;
-          ++ccount;
-          cnext = client_next_tick(cnext, d.w, S, pw);
-        }
-        if (active && k0 == 0) {
-          lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
-          lctr_add(lctr, RAFT_CTR_TO_HALTED, cnt);
+        const uint64_t heads = __ballot(active && k0 == 0);
+  #pragma unroll 1
+        for (int cs2 = 0; cs2 < CPW; ++cs2) {
+          const int b2 = cs2 * N;
+          if (!((heads >> b2) & 1)) continue;                               // wave-uniform
+          const uint32_t g2 = (uint32_t)__builtin_amdgcn_readlane((int)g, b2);
+          uint32_t cc = (uint32_t)__builtin_amdgcn_readlane((int)ccount, b2);
+          uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)cnext, b2);
+          uint32_t cnt = 0;
+          while (cn < tend) {                                               // wave-uniform
+            const uint4 d = philox(g2, P_CLIENT << 8, cc + (uint32_t)lane, 0, S.key0, S.key1);
+            uint64_t x = 1 + client_gap(d.w, pw, S.client_top);
+  #pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {                              // inclusive scan
+              const uint64_t y = (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)x, o) |
+                                 (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(x >> 32), o) << 32;
+              if (lane >= o) x += y;
+            }
+            // the injection after lane's own: its tick (lane's own fired: it is at or before
+            // the lane below's successor)
+            const uint32_t nxt = on_tick(on_index(cn, S) + x, S.client_period, S.div_burst);
+            const uint64_t stop = __ballot(nxt >= tend);
+            const int l = stop ? __builtin_ctzll(stop) : 63;                // last one fired
+            cnt += (uint32_t)l + 1;
+            cc += (uint32_t)l + 1;
+            cn = (uint32_t)__builtin_amdgcn_readlane((int)nxt, l);
+            if (stop) break;
+          }
+          if (lane >= b2 && lane < b2 + N) {
+            ccount = cc;
+            cnext = cn;
+          }
+          if (lane == b2) {
+            lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, cnt);
+            lctr_add(lctr, RAFT_CTR_TO_HALTED, cnt);
+          }
         }
       }
     }
