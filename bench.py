@@ -463,6 +463,7 @@ def run_violation(name, spec, args, world, rank, dist, make, count, total, offse
         "first_violation_tick": fv,
         "ticks_simulated": ticks,
         "time_to_first_violation_s": span_max * 1e-3,
+        "ms_per_step": span_max / max(1, ticks // spec["chunk"]),     # per chunk of ticks
         "wall_s": wall,
         "timing": "device time of the chunks (HIP events, MAX over ranks); wall_s adds the "
                   "per-chunk counter reads and all-reduces",
