@@ -541,8 +541,8 @@ def main():
             "config": head["config"],
             "roofline": head["roofline"],
         }
-        for k in ("wall_ms_per_step", "wall_value", "timing", "window", "events_per_s",
-                  "payload_evicted", "counters", "cpu_baseline"):
+        for k in ("wall_ms_per_step", "wall_value", "timing", "window", "timed_launch_ms",
+                  "timed_launches", "events_per_s", "payload_evicted", "counters", "cpu_baseline"):
             if k in head:
                 out[k] = head[k]
         if len(names) > 1:
