@@ -184,8 +184,8 @@ inline void client_powers(uint32_t client_ppm, uint64_t pw[32]) {
 // per draw at four waves per SIMD (scripts/p0_probe.hip; a loop with a load per step waited on
 // each); powers above them (client_ppm < ~2 %) take a step per loop trip first.
 constexpr int GAP_UNROLL = 12;
-template <typename T>
-__device__ inline uint64_t client_gap(uint32_t w, const T* pw, int top) {
+template <typename P>
+__device__ inline uint64_t client_gap(uint32_t w, P pw, int top) {
   // client_ppm == 0 (top == 32; reachable only through a host-written client cursor): every
   // power is 2^32, so the search takes every step
   if (top > 31) return 0xFFFFFFFFull;
@@ -214,6 +214,16 @@ __device__ inline uint64_t client_gap(uint32_t w, const T* pw, int top) {
   }
   return g;
 }
+
+// The powers' low words (DevSim::client_pw) read through the constant address space: the table is
+// written by the host only, so the compiler may load it with uniform scalar loads into SGPRs (a
+// vector load of each power held twelve VGPRs during the gap search).
+struct PowersS {
+  const __attribute__((address_space(4))) uint32_t* p;
+  __device__ explicit PowersS(const unsigned long long* pw)
+      : p((const __attribute__((address_space(4))) uint32_t*)pw) {}
+  __device__ uint32_t operator[](int i) const { return p[2 * i]; }
+};
 
 // The client schedule (SIM_SPEC §4 P0, D14): bursts of B on-ticks at the start of every period P
 // (P = 0: every tick is on). Injections are spaced by geometric gaps counted in on-ticks: the tick

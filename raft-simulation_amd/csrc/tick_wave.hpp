@@ -392,21 +392,31 @@ constexpr int cell_words() { return pair_words<N>() + (64 / N) * N * SRECW; }
 // words), for the N whose block then still fits four per CU.
 template <int N>
 constexpr bool nm_lds() { return N <= 5; }
-// TRIP_WORDS: per lane, the event ticks its cluster ran in this launch (the activity packing key);
-// DPEND_WORDS: per lane, 1 while its node's deadline is a deferred re-arm's lower bound
-// PART_WORDS: per cluster slot, the partition epoch last drawn and its draw (deliver_pack's pstate)
-constexpr int TRIP_WORDS = 64;
+// TRIP words: per cluster slot, the event ticks the cluster ran in this launch (the activity
+// packing key); DPEND_WORDS: per lane, 1 while its node's deadline is a deferred re-arm's lower
+// bound; PART words: per cluster slot, the partition epoch last drawn and its draw
+// (deliver_pack's pstate); CQ words: the client-set batch (below), per lane its injection's value
+// and the tick of the injection after it, its target node as a byte, and per cluster slot the
+// injection count the batch starts at.
+template <int N>
+constexpr int trip_words() { return 64 / N; }
 constexpr int DPEND_WORDS = 64;
-constexpr int PART_WORDS = 64;
+template <int N>
+constexpr int part_words() { return 2 * (64 / N); }
+template <int N>
+constexpr int cq_words() { return 64 + 64 + 16 + 64 / N; }
 template <int N, bool SPEC>
 constexpr int wave_lds_words() {
   return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
-         TRIP_WORDS + DPEND_WORDS + PART_WORDS;
+         trip_words<N>() + DPEND_WORDS + part_words<N>() + cq_words<N>();
 }
 template <int N, bool SPEC>
 constexpr size_t block_lds_bytes() {
-  return (PW_WORDS + wave_lds_words<N, SPEC>()) * sizeof(uint32_t);
+  return wave_lds_words<N, SPEC>() * sizeof(uint32_t);
 }
+// N <= 5 kernels run four waves per SIMD: sixteen one-wave blocks must fit the CU's 160 KB
+static_assert(block_lds_bytes<5, true>() * 16 <= 160 * 1024, "N = 5 LDS budget");
+static_assert(block_lds_bytes<4, true>() * 16 <= 160 * 1024, "N = 4 LDS budget");
 
 // SPEC selects the Spec-Raft control of SIM_SPEC §8 (variant flag 2) at compile time, so the
 // faithful kernel carries none of its code.
@@ -436,28 +446,31 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
-  // the client-gap power table (SIM_SPEC P0), then the wave's cells, counters, leader rows and
-  // per-lane words
-  uint32_t* const pw = smem;
-  if (lane < 32) pw[lane] = (uint32_t)S.client_pw[lane];
-  uint32_t* cells = smem + PW_WORDS;
+  // the wave's cells, counters, leader rows and per-lane / per-cluster words
+  uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
   uint32_t* fr = lctr + LCTR_WORDS;           // SPEC: pre-tick arena frontier per lane
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
+  // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
   uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
-  tripsL[lane] = 0;          // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
-  uint32_t* const dpend = tripsL + TRIP_WORDS;      // (likewise)
+  uint32_t* const dpend = tripsL + trip_words<N>();      // (likewise)
   dpend[lane] = 0;
   uint32_t* const pcache = dpend + DPEND_WORDS;    // [CPW] epochs, then [CPW] draws
+  uint32_t* const cq_val = pcache + part_words<N>();
+  uint32_t* const cq_nxt = cq_val + 64;
+  uint8_t* const cq_tgt = reinterpret_cast<uint8_t*>(cq_nxt + 64);
+  uint32_t* const cq_base = cq_nxt + 64 + 16;
   __builtin_amdgcn_wave_barrier();
 
   // RAFT_SCHED_ALIGNED launches a grid sized for the padded packing; waves past its slots exit.
   uint32_t wave = wave0;
   if (wave * CPW >= nslots) return;
   do {
-    if (CATCH) tripsL[lane] = 0;
-    if (lane < CPW) pcache[lane] = INF;               // no partition epoch drawn yet
+    if (lane < CPW) {
+      tripsL[lane] = 0;
+      pcache[lane] = INF;                             // no partition epoch drawn yet
+    }
     const int cs = lane / N, k0 = lane - cs * N;
     const uint32_t slot = wave * CPW + cs;      // wave slot; the cluster is perm[slot]
     const uint32_t c0 = lane < CPW * N && slot < nslots ? (perm ? perm[slot] : slot) : INF;
@@ -534,7 +547,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           uint32_t cnt = 0;
           while (cn < tend) {                                               // wave-uniform
             const uint4 d = philox(g2, P_CLIENT << 8, cc + (uint32_t)lane, 0, S.key0, S.key1);
-            uint64_t x = 1 + client_gap(d.w, pw, S.client_top);
+            uint64_t x = 1 + client_gap(d.w, PowersS(S.client_pw), S.client_top);
   #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {                              // inclusive scan
               const uint64_t y = (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)x, o) |
@@ -621,6 +634,48 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     wl_ts = __builtin_amdgcn_s_memtime();
     wl_ph[9] = (uint32_t)(wl_ts - wl_mt0);
   #endif
+    // Client-set batches. A cluster's injections are keyed by its injection count (SIM_SPEC P0),
+    // so its next N are drawn together, one per lane of the cluster: lane k draws injection
+    // count + k (target node, value, gap), an inclusive scan of (1 + gap) over the cluster's lanes
+    // gives the on-tick number of the injection after each, and the batch sits in LDS until the
+    // cluster has used it up. A refill is one wave-wide Philox pass that refills every cluster of
+    // the wave from its current count (the draws do not depend on when they are made): a wave
+    // makes about one pass per N injections of its busiest cluster instead of one per injecting
+    // trip, and the gap search and tick arithmetic go with it. P0 calls it when a cluster that
+    // injects at this trip has used its batch up; it refills the clusters whose next injection
+    // is inside the launch. (C3 first launch 68.4 -> 60.2 ms, C4-N9 17.1 -> 15.1 ms.)
+    auto refill_batch = [&](uint32_t t) {
+      if constexpr (!LITE) {
+        const uint32_t cw = (uint32_t)bl0 / N;
+        const bool want = active && cnext < tend;
+        if (__ballot(want && t == cnext && ccount - cq_base[cw] >= (uint32_t)N)) {
+          RS_PX(wl_px0);
+          const uint4 d = philox(g, P_CLIENT << 8, ccount + (uint32_t)k0, 0, S.key0, S.key1);
+          // (the table's address is opaque here so that its loads are not hoisted out of the trip
+          // loop, where the powers would hold a dozen SGPRs across every trip)
+          const unsigned long long* pwp = S.client_pw;
+          asm volatile("" : "+s"(pwp));
+          // (1 + gap) summed in 32 bits, saturating: a sum of 2^32 - 1 or more is past any tick
+          // (on_tick's never) either way
+          const uint64_t g1 = 1 + client_gap(d.w, PowersS(pwp), S.client_top);
+          uint32_t x = g1 >> 32 ? 0xFFFFFFFFu : (uint32_t)g1;
+  #pragma unroll
+          for (int o = 1; o < N; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (k0 >= o) x = x + y < x ? 0xFFFFFFFFu : x + y;
+          }
+          if (want) {
+            cq_val[lane] = d.z;
+            cq_nxt[lane] = on_tick(on_index(cnext, S) + x, S.client_period, S.div_burst);
+            cq_tgt[lane] = (uint8_t)(1 + __umulhi(d.y, N));
+            if (k0 == 0) cq_base[cw] = ccount;
+          }
+        }
+      }
+    };
+    if constexpr (!LITE) {
+      if (active && k0 == 0) cq_base[cs] = ccount - N;    // empty
+    }
     // A non-leader's re-armed timer (D4: t + el_base + the EVENT draw's word 1) is only compared
     // with ticks at or past t + el_base, so its draw is deferred (dpend) unless the event drew
     // anyway (the alts!! bit, a rand-nth redirect): the deadline holds that lower bound, which
@@ -632,7 +687,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       t = t < tend ? t : tend;
       const bool on = active && t < tend;     // the cluster has a tick to run in this trip
       if (!__ballot(on)) break;
-      if (!LITE && S.client_ppm) tripsL[lane] += on;
+      if (!LITE && S.client_ppm && k0 == 0) tripsL[(uint32_t)bl0 / N] += on;
   #ifdef RS_WAVELOG
       RS_PHASE(8);
   #endif
@@ -663,47 +718,21 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #ifdef RS_WAVELOG
       wl_inj += __ballot(cinj) ? 1 : 0;
   #endif
-      // The EVENT draw of this tick (alts!! bit, timer, rand-nth redirect) rides in the same Philox
-      // pass as the client draw: the cluster's first lane draws for the client and shares the words,
-      // and every other lane that may take a client-set without a leader id to redirect to (the
-      // redirect storm of a leaderless burst) draws its EVENT word now instead of in P1 -- one pass
-      // for both where there were two. The draw is the same one P1 would make (keyed by node and
-      // tick), so nothing but the pass count changes.
-      uint4 w = make_uint4(0, 0, 0, 0);
-      bool have_w = false;
-      if constexpr (SPEC) {                // (Spec-Raft re-arms on few events: one lane per draw)
-        if (__ballot(cinj) && cinj) {
-          RS_PX(wl_px0);
-          const uint4 d = philox(sg, P_CLIENT << 8, ccount, 0, S.key0, S.key1);
-          if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
-          if (1 + __umulhi(d.y, N) == id) {
-            inj = true;
-            injv = d.z;
-          }
-          ccount += 1;
-          cnext = client_next_tick(t, d.w, S, pw);
-        }
-      } else if (!LITE) {
+      // P0 takes the injection from the cluster's client-set batch (refill_batch above)
+      if constexpr (!LITE) {
         if (__ballot(cinj)) {
-          const bool cl = cinj && k == 0;
-          const bool ev = !cl && live && n.role != RAFT_LEADER && n.lid == 0 &&
-                          (n.rq.arr <= t || n.rq.c == 0);
-          if (cl || ev) {
-            RS_PX(wl_px0);
-            w = philox(sg, cl ? (uint32_t)P_CLIENT << 8 : id | P_EVENT << 8, cl ? ccount : t, 0,
-                       S.key0, S.key1);
-          }
-          have_w = ev;
-          const uint32_t dy = (uint32_t)__shfl((int)w.y, bl), dz = (uint32_t)__shfl((int)w.z, bl),
-                         dw = (uint32_t)__shfl((int)w.w, bl);
+          refill_batch(t);
+          const uint32_t cw = (uint32_t)bl / N;          // the cluster's wave slot
+          const uint64_t heads = __ballot(cinj && k == 0);
+          if (lane == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, (uint32_t)__popcll(heads));
           if (cinj) {
-            if (k == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, 1);
-            if (1 + __umulhi(dy, N) == id) {
+            const uint32_t s = (uint32_t)bl + (ccount - cq_base[cw]);
+            if (cq_tgt[s] == id) {
               inj = true;
-              injv = dz;
+              injv = cq_val[s];
             }
             ccount += 1;
-            cnext = client_next_tick(t, dw, S, pw);
+            cnext = cq_nxt[s];
           }
         }
       }
@@ -735,25 +764,30 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       bool elected = false, mchg = false;
       uint32_t pmax = 0;                                        // largest AE payload emitted
       uint32_t tr_cnt = 0, tr_src = 1, tr_poff = 0, tr_at = 0;   // F3 :entries capture (TRACE)
-      // A deferred timer draw due at this tick with no message ready: its own tick's draw
-      // (deadline - el_base) decides whether the node times out now.
-      if (!SPEC && live && dpend[lane] && !req_ok && !res_ok && n.deadline <= t) {
-        RS_PX(wl_px1);
-        const uint4 wd = event_draw(sg, id, n.deadline - S.el_base, S);
-        n.deadline += __umulhi(wd.y, S.el_span);
+      // The EVENT draws of this tick, in one Philox pass for the wave (the draws are keyed by
+      // cluster, node and tick, so only the pass count depends on where they are made):
+      //  - the alts!! choice (core.clj:181) when both queues are ready;
+      //  - a non-leader without a leader id that takes a REQ message: a client-set there is
+      //    redirected by rand-nth (core.clj:153-155; the redirect storm of a leaderless burst);
+      //  - a deferred timer due at this tick with no message ready: its own tick's draw
+      //    (deadline - el_base) decides whether the node times out now.
+      // The next timeout of a non-leader (core.clj:174) takes the tick's draw when there is one,
+      // else its draw is deferred (leaders' events need none).
+      uint4 w = make_uint4(0, 0, 0, 0);
+      const bool tdraw = !SPEC && live && dpend[lane] && !req_ok && !res_ok && n.deadline <= t;
+      bool have_w = (req_ok && res_ok) ||
+                    (!LITE && req_ok && n.role != RAFT_LEADER && n.lid == 0);
+      if (have_w || tdraw) {
+        RS_PX(wl_px2);
+        w = event_draw(sg, id, tdraw ? n.deadline - S.el_base : t, S);
+      }
+      if (tdraw) {
+        n.deadline += __umulhi(w.y, S.el_span);
         dpend[lane] = 0;
       }
       if (live && (req_ok || res_ok || t >= n.deadline)) {
-        // The EVENT draw is needed for the alts!! choice (core.clj:181) when both queues are ready;
-        // the next timeout of a non-leader (core.clj:174) takes it when there is one (made in P0
-        // above, or here), else its draw is deferred (leaders' events need none).
         int which = -1;
         if (req_ok && res_ok) {
-          if (!have_w) {
-            RS_PX(wl_px2);
-            w = event_draw(sg, id, t, S);
-            have_w = true;
-          }
           which = (w.x & 1) ? 1 : 0;
         } else if (req_ok) {
           which = 0;
@@ -1115,15 +1149,20 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   if constexpr (SPEC) return pv <= 0 ? 0u : ((uint32_t)pv < n.len ? (uint32_t)pv : n.len);
                   return pv > 0 ? (uint32_t)pv : 0u;
                 };
+                // (an empty log sends no prev entry: no loads, e.g. every election from init-node)
                 const uint32_t bm = n.base % A;
                 uint2 e[N];
   #pragma unroll
-                for (int p = 0; p < N; ++p) {
-                  const uint32_t prev = prev_of(p);
-                  const uint32_t at = SPEC ? (prev ? prev - 1 : 0u) : (prev < n.len ? prev : 0u);
-                  uint32_t slot = bm + at;
-                  slot = slot >= A ? slot - A : slot;
-                  e[p] = sar[slot];
+                for (int p = 0; p < N; ++p) e[p] = make_uint2(0, 0);
+                if (n.len) {
+  #pragma unroll
+                  for (int p = 0; p < N; ++p) {
+                    const uint32_t prev = prev_of(p);
+                    const uint32_t at = SPEC ? (prev ? prev - 1 : 0u) : (prev < n.len ? prev : 0u);
+                    uint32_t slot = bm + at;
+                    slot = slot >= A ? slot - A : slot;
+                    e[p] = sar[slot];
+                  }
                 }
   #pragma unroll
                 for (int p = 1; p <= N; ++p) {
@@ -1558,7 +1597,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       const uint32_t key = !head ? INF
                            : S.client_ppm
                                ? (dead ? SCHED_BUCKETS - 1
-                                       : SCHED_BUCKETS - 2 - min(tripsL[lane], SCHED_BUCKETS - 2))
+                                       : SCHED_BUCKETS - 2 - min(tripsL[cs], SCHED_BUCKETS - 2))
                                : sched_bucket(cm, tend);
       if (head) S.skey[c] = key;
       // a packed wave's clusters usually share their next key: one histogram atomic for the wave

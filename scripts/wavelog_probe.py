@@ -1,6 +1,6 @@
 """Per-wave timeline of one general-kernel launch from a -DRS_WAVELOG build (diagnostic only):
 lifetime distribution, start-time generations, per-CU/SIMD packing, per-phase shader cycles.
-Usage: wavelog_probe.py LIB [clusters] [c3|c3_spec|c4_n9|c4_spec] [launches]"""
+Usage: wavelog_probe.py LIB [clusters] [c2|c3|c3_spec|c4_n9|c4_spec] [launches]"""
 import ctypes
 import sys
 from pathlib import Path
@@ -18,7 +18,7 @@ C3 = dict(nodes=5, seed=1, log_cap=256, client_ppm=80000, client_period=16384, c
           client_redirects=4, drop_ppm=100000, dup_ppm=10000, dmin=1, dmax=50, part_ppm=100000)
 C4 = dict(nodes=9, seed=5, log_cap=4096, client_ppm=500000, client_period=8192, client_burst=2048,
           client_redirects=4)
-CFG = {"c3": C3, "c3_spec": dict(C3, variant_flags=2, log_cap=1024), "c4_n9": C4,
+CFG = {"c2": dict(nodes=5, seed=42), "c3": C3, "c3_spec": dict(C3, variant_flags=2, log_cap=1024), "c4_n9": C4,
        "c4_spec": dict(C4, variant_flags=2)}[WL]
 LAUNCHES = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 sim = Backend(lib, "raft_sim_", n_clusters=C, **CFG)
