@@ -95,6 +95,22 @@ struct DevSim {
   uint32_t* bail_report;    // host-mapped word (the host picks the next launches' path from it)
 };
 
+// The kernel's DevSim argument, read where a field is used. The kernels that run the tick body
+// (tick_kernel, steady_lane_kernel) take their DevSim unmodified as the first argument, at offset
+// 0 of the kernarg segment. A field read through this opaque constant-address pointer is a scalar
+// load at its use; read from the plain parameter it is loaded once and held in an SGPR across the
+// trip loop, whose uniform values exceed the SGPR file (the excess is spilled to VGPR lanes and
+// costs a v_readlane at every use and two VGPRs). For the fields the trip loop uses rarely.
+using KDevSim = const __attribute__((address_space(4))) DevSim;
+__device__ __forceinline__ KDevSim* kargs() {
+  KDevSim* p = (KDevSim*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ DivU32 kdiv(const __attribute__((address_space(4))) DivU32& v) {
+  return DivU32{v.d, v.m, v.s1, v.s2};
+}
+
 // A cluster block: the cluster's 8 words (hot_cl_off = 0), then the node fields, field-major
 // (word HOT_CW + f * N + k is field f of node k): the HotField fields, next_index of peer id p as
 // field HF_NEXT + p - 1, match_index as HF_NEXT + N + p - 1, then the arena cursors and the

@@ -42,24 +42,26 @@ template <bool LITE>
 __device__ __forceinline__ uint32_t deliver_pack(const DevSim& S, uint32_t g, uint32_t t,
                                                  uint32_t src, uint32_t id, uint32_t pstate,
                                                  uint32_t* lctr) {
-  if (LITE || (!S.drop_ppm && !S.dup_ppm && !S.part_ppm && S.dmin == S.dmax))
-    return S.dmin | 1u << 16;
+  if (LITE) return S.dmin | 1u << 16;
+  KDevSim* const K = kargs();
+  const uint32_t drop = K->drop_ppm, dup = K->dup_ppm, dmin = K->dmin, dmax = K->dmax;
+  if (!drop && !dup && !K->part_ppm && dmin == dmax) return dmin | 1u << 16;
   // pstate: the cluster's partition draw of this epoch (bit 0: partitioned, bit i: node i's side)
   if ((pstate & 1) && (((pstate >> id) ^ (pstate >> src)) & 1)) {
     lctr_add(lctr, RAFT_CTR_PARTITIONED, 1);
     return 0;
   }
-  if (!S.drop_ppm && !S.dup_ppm && S.dmin == S.dmax) return S.dmin | 1u << 16;
+  if (!drop && !dup && dmin == dmax) return dmin | 1u << 16;
   const uint4 w = philox(g, src | P_NET << 8, t, id, S.key0, S.key1);
-  if (ppm(w.x) < S.drop_ppm) {
+  if (ppm(w.x) < drop) {
     lctr_add(lctr, RAFT_CTR_DROPPED, 1);
     return 0;
   }
-  const uint32_t span = S.dmax - S.dmin + 1;
-  uint32_t pack = (S.dmin + __umulhi(w.z, span)) | 1u << 16;
-  if (ppm(w.y) < S.dup_ppm) {
+  const uint32_t span = dmax - dmin + 1;
+  uint32_t pack = (dmin + __umulhi(w.z, span)) | 1u << 16;
+  if (ppm(w.y) < dup) {
     lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
-    pack = (pack & 0xFF) | (S.dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
+    pack = (pack & 0xFF) | (dmin + __umulhi(w.w, span)) << 8 | 2u << 16;
   }
   return pack;
 }
@@ -206,9 +208,9 @@ __device__ __forceinline__ void spec_handle(
   if (type == RAFT_MSG_APPEND_ENTRIES && mterm >= n.term) {
     consistent = mb == 0;
     if (!consistent && mb <= n.len && mep) consistent = sar[(n.base + mb - 1) % A].x == met;
-    if (consistent && mb + pcnt > S.L) fault = RAFT_FAULT_OVERFLOW;
+    if (consistent && mb + pcnt > kargs()->L) fault = RAFT_FAULT_OVERFLOW;
   }
-  if (type == RAFT_MSG_CLIENT_SET && n.role == RAFT_LEADER && n.len + 1 > S.L)
+  if (type == RAFT_MSG_CLIENT_SET && n.role == RAFT_LEADER && n.len + 1 > kargs()->L)
     fault = RAFT_FAULT_OVERFLOW;
   if (fault) return;
   if (type != RAFT_MSG_CLIENT_SET && mterm > n.term) {          // term rule: step down
@@ -219,7 +221,7 @@ __device__ __forceinline__ void spec_handle(
     case RAFT_MSG_REQUEST_VOTE: {
       const uint32_t lt = n.len ? sar[(n.base + n.len - 1) % A].x : 0u;
       const uint32_t mt = mep ? met : 0u;
-      const bool up = (S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) || mt > lt ||
+      const bool up = (kargs()->variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) || mt > lt ||
                       (mt == lt && ma >= n.len);
       const uint32_t grant = mterm == n.term && (n.vf == 0 || n.vf == src) && up;
       ra = make_uint4(RAFT_MSG_VOTE_RESPONSE | id << 3 | grant << 7, n.term, 0, 0);
@@ -535,7 +537,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // run (SIM_SPEC P0; the Spec-Raft control's client-sets reach halted nodes the same way).
     if constexpr (!LITE) {
       const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
-      if (S.client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
+      if (kargs()->client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
         const uint64_t heads = __ballot(active && k0 == 0);
   #pragma unroll 1
         for (int cs2 = 0; cs2 < CPW; ++cs2) {
@@ -651,13 +653,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         if (__ballot(want && t == cnext && ccount - cq_base[cw] >= (uint32_t)N)) {
           RS_PX(wl_px0);
           const uint4 d = philox(g, P_CLIENT << 8, ccount + (uint32_t)k0, 0, S.key0, S.key1);
-          // (the table's address is opaque here so that its loads are not hoisted out of the trip
-          // loop, where the powers would hold a dozen SGPRs across every trip)
-          const unsigned long long* pwp = S.client_pw;
-          asm volatile("" : "+s"(pwp));
+          // (the fields by scalar loads here: kargs)
+          KDevSim* const K = kargs();
           // (1 + gap) summed in 32 bits, saturating: a sum of 2^32 - 1 or more is past any tick
           // (on_tick's never) either way
-          const uint64_t g1 = 1 + client_gap(d.w, PowersS(pwp), S.client_top);
+          const uint64_t g1 = 1 + client_gap(d.w, PowersS(K->client_pw), K->client_top);
           uint32_t x = g1 >> 32 ? 0xFFFFFFFFu : (uint32_t)g1;
   #pragma unroll
           for (int o = 1; o < N; o <<= 1) {
@@ -666,7 +666,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           }
           if (want) {
             cq_val[lane] = d.z;
-            cq_nxt[lane] = on_tick(on_index(cnext, S) + x, S.client_period, S.div_burst);
+            const uint32_t P = K->client_period;
+            const DivU32 dp = kdiv(K->div_period), db = kdiv(K->div_burst);
+            const uint32_t q = P ? udiv(dp, cnext) : 0u;
+            const uint64_t oi = P ? (uint64_t)q * db.d + (cnext - q * P) : cnext;   // on_index
+            cq_nxt[lane] = on_tick(oi + x, P, db);
             cq_tgt[lane] = (uint8_t)(1 + __umulhi(d.y, N));
             if (k0 == 0) cq_base[cw] = ccount;
           }
@@ -687,7 +691,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       t = t < tend ? t : tend;
       const bool on = active && t < tend;     // the cluster has a tick to run in this trip
       if (!__ballot(on)) break;
-      if (!LITE && S.client_ppm && k0 == 0) tripsL[(uint32_t)bl0 / N] += on;
+      if (!LITE && k0 == 0 && kargs()->client_ppm) tripsL[(uint32_t)bl0 / N] += on;
   #ifdef RS_WAVELOG
       RS_PHASE(8);
   #endif
@@ -779,10 +783,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                     (!LITE && req_ok && n.role != RAFT_LEADER && n.lid == 0);
       if (have_w || tdraw) {
         RS_PX(wl_px2);
-        w = event_draw(sg, id, tdraw ? n.deadline - S.el_base : t, S);
+        w = event_draw(sg, id, tdraw ? n.deadline - kargs()->el_base : t, S);
       }
       if (tdraw) {
-        n.deadline += __umulhi(w.y, S.el_span);
+        n.deadline += __umulhi(w.y, kargs()->el_span);
         dpend[lane] = 0;
       }
       if (live && (req_ok || res_ok || t >= n.deadline)) {
@@ -897,7 +901,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           switch (type) {
             case RAFT_MSG_REQUEST_VOTE: {                     // request-vote-handler 91-103
               uint32_t consistent = 1;
-              if (!(S.variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) && ma != 0) {
+              if (!(kargs()->variant & RAFT_VARIANT_VOTE_NO_LOG_CHECK) && ma != 0) {
                 if (ma > n.len) {
                   fault = RAFT_FAULT_IOOBE;
                   break;
@@ -928,7 +932,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 n.len = n.len > mb ? n.len - mb : 0;          // remove-from! 78-81
                 n.seq = 1;
               } else {
-                if (n.len + pcnt > S.L) {
+                if (n.len + pcnt > kargs()->L) {
                   fault = RAFT_FAULT_OVERFLOW;
                   break;
                 }
@@ -962,7 +966,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 emit = 4;
                 break;
               }
-              if (n.len + 1 > S.L) {
+              if (n.len + 1 > kargs()->L) {
                 fault = RAFT_FAULT_OVERFLOW;
                 break;
               }
@@ -1040,14 +1044,15 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // (D4); Spec-Raft keeps Raft's timers (SIM_SPEC §8)
           if (n.role == RAFT_LEADER) {
             if (!SPEC || ev == 7 || elected) {
-              n.deadline = t + S.hb;
+              n.deadline = t + kargs()->hb;
               dpend[lane] = 0;
             }
           } else if (!SPEC || ev == 6 || rearm || was_leader) {
             // Spec-Raft re-arms on few events (SIM_SPEC §8): drawn at once there
             if (SPEC && !have_w) w = event_draw(sg, id, t, S);
             const bool defer = !SPEC && !have_w;
-            n.deadline = t + S.el_base + (defer ? 0u : __umulhi(w.y, S.el_span));
+            KDevSim* const K = kargs();
+            n.deadline = t + K->el_base + (defer ? 0u : __umulhi(w.y, K->el_span));
             if (!SPEC) dpend[lane] = defer;                    // the draw is deferred
             have_w = have_w || SPEC;
           }
@@ -1086,7 +1091,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
           if (!LITE && emit == 4) {
             emit = 0;
-            if (mb >= S.client_redirects) {
+            if (mb >= kargs()->client_redirects) {
               lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
             } else {
               uint32_t dst = n.lid;
@@ -1114,14 +1119,16 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           if (emit) {
             // the cluster's partition draw for this tick's epoch, made once per epoch (SIM_SPEC P2)
             uint32_t pstate = 0;
-            if (!LITE && S.part_ppm) {
+            if (!LITE && kargs()->part_ppm) {
               const int cw = bl / N;
-              const uint32_t e = udiv(S.div_epoch, t);
+              KDevSim* const K = kargs();
+              const DivU32 de = kdiv(K->div_epoch);
+              const uint32_t e = udiv(de, t);
               pstate = pcache[CPW + cw];
               if (pcache[cw] != e) {
                 RS_PX(wl_px5);
                 const uint4 pw = philox(sg, P_PART << 8, e, 0, S.key0, S.key1);
-                pstate = (pw.y & ~1u) | (ppm(pw.x) < S.part_ppm ? 1u : 0u);
+                pstate = (pw.y & ~1u) | (ppm(pw.x) < K->part_ppm ? 1u : 0u);
                 pcache[cw] = e;          // (the cluster's lanes that draw write the same words)
                 pcache[CPW + cw] = pstate;
               }
@@ -1274,17 +1281,20 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           }
         }
         if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
-          uint32_t cc = S.ccount[sgi];
-          if (S.SC) {
-            uint32_t si = (n.base + n.commit - papplied) % A, so = cc % S.SC;
-            uint32_t* const ring = S.stream + (size_t)sgi * S.SC;
+          KDevSim* const K = kargs();
+          uint32_t* const cca = K->ccount;
+          const uint32_t SC = K->SC;
+          uint32_t cc = cca[sgi];
+          if (SC) {
+            uint32_t si = (n.base + n.commit - papplied) % A, so = cc % SC;
+            uint32_t* const ring = K->stream + (size_t)sgi * SC;
             for (uint32_t i = 0; i < papplied; ++i) {
               ring[so] = sar[si].y;
               si = si + 1 == A ? 0 : si + 1;
-              so = so + 1 == S.SC ? 0 : so + 1;
+              so = so + 1 == SC ? 0 : so + 1;
             }
           }
-          S.ccount[sgi] = cc + papplied;
+          cca[sgi] = cc + papplied;
         }
         if constexpr (TRACE) {   // the traced message's :entries, resolved like the payload above
           const uint32_t tfront = __shfl(n.front, bl + (int)tr_src - 1);
@@ -1434,7 +1444,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // traffic a cluster has an event nearly every tick of a burst: measured C3 +3 % with one
       // wave-wide clock, unchanged with per-cluster clocks, C4-N9 +1 %), and it would cost the
       // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
-      if constexpr (!SPEC && !TRACE && N <= 5) if (LITE || !S.client_ppm) {
+      if constexpr (!SPEC && !TRACE && N <= 5) if (LITE || !kargs()->client_ppm) {
         // leaders whose responses can drain: a log past the hwm makes a success response a
         // checker event (C3/C4 replication), so those leaders stay with the loop
         const bool elig = on && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;
@@ -1487,7 +1497,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   } else {                                   // 143-144: (dec next-index)
                     lsw.next(src - 1) -= 1;
                   }
-                  n.deadline = tau + S.hb;
+                  n.deadline = tau + kargs()->hb;
                   n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
                                         n.term, 0);
                   lctr_add(lctr, RAFT_CTR_EV_AR, 1);
@@ -1535,7 +1545,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 } else {                                     // 143-144: (dec next-index)
                   lsw.next(src - 1) -= 1;
                 }
-                n.deadline = tau + S.hb;
+                n.deadline = tau + kargs()->hb;
                 n.trace = trace_event(n.trace, tau, RAFT_MSG_APPEND_RESPONSE, src, mterm, n.role,
                                       n.term, 0);
                 lctr_add(lctr, RAFT_CTR_EV_AR, 1);
@@ -1579,7 +1589,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // a deferred draw stays owed in the stored state (FL_DRAW, device.hpp)
     const uint32_t owed = !SPEC && active && dpend[lane] ? FL_DRAW : 0u;
     if (!SPEC) dpend[lane] = 0;
-    if (S.shist) {
+    KDevSim* const KW = kargs();
+    if (KW->shist) {
       // RAFT_SCHED_ALIGNED: the cluster's packing key relative to the next launch, counted into the
       // bucket histogram the host turns into the next launch's wave packing (sched_range_kernel)
       const uint32_t me = active && !n.fault ? sched_key_of(n.deadline, n.rq, n.rs) : INF;
@@ -1595,18 +1606,18 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // packs into waves of their own and runs without trips (below the state load).
       const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
       const uint32_t key = !head ? INF
-                           : S.client_ppm
+                           : KW->client_ppm
                                ? (dead ? SCHED_BUCKETS - 1
                                        : SCHED_BUCKETS - 2 - min(tripsL[cs], SCHED_BUCKETS - 2))
                                : sched_bucket(cm, tend);
-      if (head) S.skey[c] = key;
+      if (head) KW->skey[c] = key;
       // a packed wave's clusters usually share their next key: one histogram atomic for the wave
       const uint32_t kmin = wave_min(key), kmax = ~wave_min(head ? ~key : ~0u);
       const uint32_t heads = (uint32_t)__popcll(__ballot(head));   // (ballot outside any branch)
       if (kmin == kmax) {
-        if (lane == 0 && kmin != INF) atomicAdd(&S.shist[kmin], heads);
+        if (lane == 0 && kmin != INF) atomicAdd(&KW->shist[kmin], heads);
       } else if (head) {
-        atomicAdd(&S.shist[key], 1u);
+        atomicAdd(&KW->shist[key], 1u);
       }
     }
     if (active) {
@@ -1639,7 +1650,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     }
   } while (CATCH && (wave += wstride) * CPW < nslots);   // the general grid covers every slot
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  unsigned long long* const ctr = S.ctr + (size_t)(ctr_copy % CTR_COPIES) * CTR_STRIDE;
+  unsigned long long* const ctr = kargs()->ctr + (size_t)(ctr_copy % CTR_COPIES) * CTR_STRIDE;
   if (lane < RAFT_CTR_COUNT) {
     const uint32_t v = lctr[lane];
     if (v) atomicAdd(&ctr[lane], (unsigned long long)v);
