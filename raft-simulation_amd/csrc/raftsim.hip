@@ -81,8 +81,9 @@ struct Shard {
   // Path choice per launch (speed only: both paths give the same state). RAFTSIM_STEADY=auto
   // (default): the steady kernel unless the last catch-up launch the host has seen (bail_host,
   // written by the GPU; a few launches stale at most) took more than 1/16 of the clusters, then
-  // the general kernel for the next STEADY_COOLDOWN launches; the first launch of a handle
-  // (init-node: every cluster still has to elect) is general. "always" / "never" force a path.
+  // the general kernel for the next STEADY_COOLDOWN launches. The first launch of a handle is
+  // steady too: the steady kernel runs init-node's election in closed form (steady_kernel.hip).
+  // "always" / "never" force a path.
   int steady_mode;                     // 0 auto, 1 always, 2 never
   uint32_t* bail_host;                 // host-mapped word (hipHostMalloc)
   uint32_t steady_cooldown;
@@ -250,7 +251,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     const char* m = getenv("RAFTSIM_STEADY");
     s->steady_mode = m && !strcmp(m, "always") ? 1 : m && !strcmp(m, "never") ? 2 : 0;
 
-    s->steady_cooldown = 1;
+    s->steady_cooldown = 0;
     void* hp = nullptr;
     if (hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d.bail_report), hp, 0) != hipSuccess) {

@@ -319,6 +319,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   const uint32_t tend = t0 + nt, d = S.dmin;
   const uint32_t P = 2 * d + F - 1 + S.hb, allF = (1u << F) - 1;
   uint32_t dl = 0, nhb = 0, nae = 0, nar = 0;  // lines of the block changed; events run
+  bool el = false;                             // the cluster's election ran here (general path)
 #ifdef RS_WAVELOG
   uint64_t wl_x1 = 0, wl_x2 = 0, wl_x3 = 0, wl_lend = 0;
 #endif
@@ -483,6 +484,111 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #pragma unroll
       for (int k = 0; k < N; ++k) out[k] = w[HOT_CW + f * N + k];
     };
+    // ------------------------------------------- the election from init-node, in closed form
+    // A cluster still in init-node's state (core.clj:31-38: every node a follower of the same term
+    // with no vote, leader, log, leader-state or message; no checker mark) elects the node whose
+    // timer fires first, and with no faults, no client and a fixed delay d that election is one
+    // script when no other timer fires before the request-vote reaches it (D_k >= t1 + d):
+    //   t1            candidate c times out (timeout-handler 166-169): term T + 1, request-vote
+    //                 to every peer;
+    //   t1 + d        every follower grants it (request-vote-handler 91-103: vote, no term change);
+    //   t1 + 2d + i   c takes the i-th vote response in sender order (vote-response-handler
+    //                 125-139) and is leader at the one that makes a majority (i_L), broadcasting
+    //                 an empty append-entries (candidate->leader 80-84, append-entries-rpc 56-67);
+    //   tL + d        every follower takes it (append-entries-handler 105-123: term T + 1, :follwer,
+    //                 leader id) and answers; c takes the rest of the votes, then the F responses
+    //                 one per tick from max(t1 + 2d + F, tL + 2d) (append-response-handler 141-149).
+    // Every timer re-arm is one the general body defers (followers' draws stay owed), the leader's
+    // rows end as init-node's (next = mb = 0, match = 0) and nothing is left queued: the script
+    // writes the cluster's state after its last event into the registers below, and the cluster is
+    // then at the fixed point, which the rest of this path runs to the launch's end (trace hashes,
+    // deadlines and counters as the general body gives them). Anything else -- ties, an election
+    // cut by the launch's end, a state that only looks like init-node -- is bailed as before.
+    {
+      auto ifield = [&](int f, int k) { return w[HOT_CW + f * N + k]; };
+      bool pat = active && w[0] == 0 && S.Q >= 2u * F && S.el_base >= P && S.hb >= 2 * d + F;
+      const uint32_t T = ifield(HF_TERM, 0);
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        pat = pat && ifield(HF_FLAGS, k) == 0 && ifield(HF_MASKS, k) == 0 &&
+              ifield(HF_TERM, k) == T && ifield(HF_COMMIT, k) == 0 && ifield(HF_LEN, k) == 0 &&
+              ifield(HF_QMETA, k) == 0 && ifield(HF_REQ_ARR, k) == INF &&
+              ifield(HF_RES_ARR, k) == INF;
+#pragma unroll
+        for (int p = 0; p < 2 * N; ++p) pat = pat && ifield(HF_NEXT + p, k) == 0;
+      }
+      pat = pat && T != INF;
+      // the candidate: the unique earliest deadline, every other one at least d later
+      uint32_t cidx = 0, t1 = INF;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const uint32_t dk = ifield(HF_DEADLINE, k);
+        cidx = dk < t1 ? (uint32_t)k : cidx;
+        t1 = min(t1, dk);
+      }
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        pat = pat && ((uint32_t)k == cidx || (uint64_t)ifield(HF_DEADLINE, k) >= (uint64_t)t1 + d);
+      constexpr uint32_t iL = (N + 1) / 2 >= 2 ? (N + 1) / 2 - 2 : 0;   // the electing response
+      const uint64_t tL = (uint64_t)t1 + 2 * d + iL;
+      const uint64_t tau0 = max((uint64_t)t1 + 2 * d + F, tL + 2 * d);  // the first response
+      const uint64_t tlast = tau0 + F - 1;
+      pat = pat && t1 >= t0 && tlast < tend;
+      // the election-safety check (P4) compares the new leader's led term with the others'
+      // (words past the image: read only when some cluster of the wave qualifies)
+      if (__builtin_amdgcn_ballot_w64(pat)) {                 // wave-uniform
+        const uint32_t* lp = S.hot + (size_t)c * HB + HOT_CW + hf_led(N) * N;
+        uint32_t led[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) led[k] = lp[k];
+#pragma unroll
+        for (int k = 0; k < N; ++k) pat = pat && ((uint32_t)k == cidx || led[k] != T + 1);
+      }
+      if (pat) {
+        el = true;
+        const uint32_t T1 = T + 1, cid = cidx + 1;
+        // the candidate's events (node cidx), then each follower's
+        uint64_t hc = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if ((uint32_t)k == cidx)
+            hc = (uint64_t)ifield(HF_TRACE_HI, k) << 32 | ifield(HF_TRACE_LO, k);
+        hc = trace_event(hc, t1, 6, 0, 0, RAFT_CANDIDATE, T1, 0);
+#pragma unroll
+        for (int i = 0; i < F; ++i) {
+          const uint32_t sid = (uint32_t)i + ((uint32_t)i >= cidx ? 2u : 1u);   // slot i's id
+          hc = trace_event(hc, t1 + 2 * d + i, RAFT_MSG_VOTE_RESPONSE, sid, T,
+                           (uint32_t)i >= iL ? RAFT_LEADER : RAFT_CANDIDATE, T1, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const uint32_t sid = (uint32_t)j + ((uint32_t)j >= cidx ? 2u : 1u);
+          hc = trace_event(hc, (uint32_t)tau0 + j, RAFT_MSG_APPEND_RESPONSE, sid, T, RAFT_LEADER,
+                           T1, 0);
+        }
+        const uint32_t peers = ((1u << (N + 1)) - 1) & ~1u & ~(1u << cid);
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          const bool isc = (uint32_t)k == cidx;
+          uint64_t h = (uint64_t)ifield(HF_TRACE_HI, k) << 32 | ifield(HF_TRACE_LO, k);
+          h = trace_event(h, t1 + d, RAFT_MSG_REQUEST_VOTE, cid, T1, RAFT_FOLLOWER, T, 0);
+          h = trace_event(h, (uint32_t)tL + d, RAFT_MSG_APPEND_ENTRIES, cid, T1, RAFT_FOLLWER, T1, 0);
+          h = isc ? hc : h;
+          w[HOT_CW + HF_FLAGS * N + k] = isc ? pack_flags(RAFT_LEADER, 0, cid, 0, 0, 1)
+                                             : pack_flags(RAFT_FOLLWER, 0, cid, 0, 0, 0) | FL_DRAW;
+          w[HOT_CW + HF_MASKS * N + k] = isc ? peers << 16 : 0u;
+          w[HOT_CW + HF_TERM * N + k] = T1;
+          w[HOT_CW + HF_DEADLINE * N + k] = isc ? (uint32_t)tlast + S.hb
+                                                : (uint32_t)tL + d + S.el_base;   // + the owed draw
+          w[HOT_CW + HF_REQ_TAIL * N + k] = 0;
+          w[HOT_CW + HF_RES_TAIL * N + k] = 0;
+          w[HOT_CW + HF_TRACE_LO * N + k] = (uint32_t)h;
+          w[HOT_CW + HF_TRACE_HI * N + k] = (uint32_t)(h >> 32);
+        }
+        nae = F;                                    // the followers' append-entries and their
+        nar = F;                                    // responses (the rest is counted as nel)
+      }
+    }
     uint32_t nfl[N], nqm[N];
     field(HF_FLAGS, nfl);
     field(HF_QMETA, nqm);
@@ -1028,7 +1134,8 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         pend &= ~same;
       }
     }
-    const bool wfp = !__builtin_amdgcn_ballot_w64(wb && !fp);
+    // (a cluster that ran its election here changed flags, masks and terms too)
+    const bool wfp = !__builtin_amdgcn_ballot_w64(wb && (!fp || el));
     if (wb) {
       // every word of fields DEADLINE..LEN, from registers (LEN unchanged)
       constexpr int NV = HF_NEXT;
@@ -1080,6 +1187,18 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           *lds_at<uint4>(img, img_off(lane, i)) = x;
           dl |= (uint32_t)(x.x != w[q] || x.y != w[q + 1] || x.z != w[q + 2] || x.w != w[q + 3])
                 << (i / 8);
+        }
+      }
+      if (el) {
+        // the words the election changed are compared with the registers it wrote: its lines are
+        // dirty; and the new leader's led term (P4), in the image or past it
+        dl |= (1u << ((HOT_CW + HF_NEXT * N + 31) / 32)) - 1;
+        const uint32_t q = HOT_CW + hf_led(N) * N + L;
+        if (q < (uint32_t)IMGC * 4) {
+          *lds_at<uint32_t>(img, img_off(lane, q / 4) + 4 * (q % 4)) = Lterm;
+          dl |= 1u << (q / 32);
+        } else {
+          S.hot[(size_t)c * HB + q] = Lterm;
         }
       }
       // the steady certificate for the next launch: the cluster stays at its fixed point
@@ -1179,15 +1298,21 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #endif
   // counters: heartbeats, append-entries, append-responses; every message is delivered. One
   // wave-wide sum each, added by five lanes to the wave's copy of the counter block.
+  // Elections run here add a timeout, F request-votes and F vote responses, a leader, and the
+  // request-vote, vote-response and append-entries messages (3F; the responses are in a).
   {
     const uint32_t h = wave_sum(nhb), a = wave_sum(nae), r = wave_sum(nar);
+    const uint32_t ne = wave_sum(el ? 1u : 0u);
     unsigned long long* const ctr =
         S.ctr + (size_t)((blockIdx.x * 4 + wave) % CTR_COPIES) * CTR_STRIDE;
-    if (lane < 5) {
-      const uint32_t msgs = (uint32_t)F * h + a;
+    if (lane < 9) {
+      const uint32_t msgs = (uint32_t)F * h + a + 3u * F * ne;
       const int idx = lane == 0 ? RAFT_CTR_EV_HEARTBEAT : lane == 1 ? RAFT_CTR_EV_AE
-                    : lane == 2 ? RAFT_CTR_EV_AR : lane == 3 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
-      const uint32_t v = lane == 0 ? h : lane == 1 ? a : lane == 2 ? r : msgs;
+                    : lane == 2 ? RAFT_CTR_EV_AR : lane == 3 ? RAFT_CTR_SENT
+                    : lane == 4 ? RAFT_CTR_DELIVERED : lane == 5 ? RAFT_CTR_EV_TIMEOUT
+                    : lane == 6 ? RAFT_CTR_EV_RV : lane == 7 ? RAFT_CTR_EV_VR : RAFT_CTR_LEADERS;
+      const uint32_t v = lane == 0 ? h : lane == 1 ? a : lane == 2 ? r : lane <= 4 ? msgs
+                       : lane == 5 || lane == 8 ? ne : (uint32_t)F * ne;
       if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
     }
   }

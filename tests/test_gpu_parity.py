@@ -144,8 +144,10 @@ def test_gpu_matches_oracle(name):
 def test_gpu_c2_full_size(seed):
     """BASELINE config 2: 65,536 five-node clusters, no faults, for the seeds of SURVEY §8(d) and
     one above 2^32 (Philox key word 1 nonzero): digest-equal after each of four 10k-tick launches.
-    The first launch (elections) runs the general kernel; the last one is the steady kernel alone
-    on the 256-workgroup grid with no cluster bailed (core.clj:105-123,141-149,162-164)."""
+    The first launch (elections) runs the steady kernel, which runs init-node's election in closed
+    form and hands the clusters it cannot (two timers within d of each other: under 0.2 %) to the
+    general body; the last one is the steady kernel alone on the 256-workgroup grid with no cluster
+    bailed (core.clj:91-139,105-123,141-149,162-169)."""
     cfg = dict(n_clusters=65536, nodes=5, seed=seed)
     g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
     helpers.oracle_threads(r, helpers.cpu_threads())
@@ -157,7 +159,29 @@ def test_gpu_c2_full_size(seed):
         bad = np.nonzero(g.digest() != r.digest())[0]
         assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
     assert g.counters() == r.counters()
-    assert bails[0] == -1 and bails[-1] == 0, bails
+    assert 0 <= bails[0] < 65536 // 500 and bails[-1] == 0, bails
+
+
+@pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
+def test_gpu_init_election_closed_form(nodes, d):
+    """The steady kernel's election from init-node (steady_kernel.hip) for every follower count
+    and a delay above 1 (the electing vote response and the first append-response tick move with
+    both): short timers so that elections, the first heartbeat rounds and the ties it hands to the
+    general body all fall inside the first launch; digest- and counter-equal to the oracle after
+    each launch, with few clusters bailed (core.clj:91-139,166-169)."""
+    cfg = dict(n_clusters=16384, nodes=nodes, seed=7 + nodes, hb=300, el_base=700, el_span=900,
+               dmin=d, dmax=d)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    bails = []
+    for launch in range(3):
+        g.step(3000)
+        r.step(3000)
+        bails.append(g.diag_last_bails())
+        bad = np.nonzero(g.digest() != r.digest())[0]
+        assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
+    assert g.counters() == r.counters()
+    assert 0 <= bails[0] < 16384 // 20, bails
 
 
 def _client_set_into(be, cluster, node, value):
@@ -421,7 +445,29 @@ def test_gpu_steady_path_taken():
         bails.append(g.diag_last_bails())
         assert (g.digest() == r.digest()).all()
     assert g.counters() == r.counters()
-    assert bails[0] == -1 and bails[-1] == 0, bails
+    assert 0 <= bails[0] < 65536 // 500 and bails[-1] == 0, bails
+
+
+@pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
+def test_gpu_init_election_closed_form(nodes, d):
+    """The steady kernel's election from init-node (steady_kernel.hip) for every follower count
+    and a delay above 1 (the electing vote response and the first append-response tick move with
+    both): short timers so that elections, the first heartbeat rounds and the ties it hands to the
+    general body all fall inside the first launch; digest- and counter-equal to the oracle after
+    each launch, with few clusters bailed (core.clj:91-139,166-169)."""
+    cfg = dict(n_clusters=16384, nodes=nodes, seed=7 + nodes, hb=300, el_base=700, el_span=900,
+               dmin=d, dmax=d)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    bails = []
+    for launch in range(3):
+        g.step(3000)
+        r.step(3000)
+        bails.append(g.diag_last_bails())
+        bad = np.nonzero(g.digest() != r.digest())[0]
+        assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
+    assert g.counters() == r.counters()
+    assert 0 <= bails[0] < 16384 // 20, bails
 
 
 LITE_CASES = ["c2_small", "lite_n2", "lite_n3", "lite_n4", "lite_elections", "lite_tiny_inbox",
