@@ -1333,42 +1333,84 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // a position with the same term and another value. The appenders' (appended_at, base,
           // len) go through LDS (the cells: P2 is done with them) so a lane can read any
           // appender's words from inside the divergent loop.
+          // Copies of one payload: a payload append's entry at position p comes from its sender's
+          // arena slot key + p (key = source offset - appended_at; evicted ones read (0, 0) the
+          // same way, SIM_SPEC P3), so two nodes that appended payloads of the same sender with the
+          // same key in this tick hold the same entries where both appended (no write this tick
+          // reaches a slot that is not evicted). A lane therefore compares one member of each group
+          // of appenders with the same (sender, key, appended_at, len) and gives the group its
+          // result, and skips positions where it appended a copy of the same payload itself: the
+          // followers of a broadcast that all appended the leader's entries in one tick cost one
+          // comparison per lane instead of one per follower (C4). Only with a fixed delay, where a
+          // broadcast's copies land in one tick (with random delays they rarely do), as separate
+          // code (sharing the loop with the plain form cost C3's kernel 2 % in registers).
           uint32_t* const apw = cells;
           apw[lane] = (uint32_t)appended_at;
           apw[64 + lane] = n.base;
           apw[128 + lane] = n.len;
-          __builtin_amdgcn_wave_barrier();
           const uint32_t apc = (uint32_t)(__ballot(active && appended_at >= 0) >> bl) & cmask;
-          uint32_t todo = active ? apc & ~(1u << k) : 0u;
-          uint32_t found = 0, cur = 0, rem = 0, xi = 0, yi = 0;
-          const uint2* xa = sar;
           constexpr int W = LITE ? 1 : 8;
-          while (__ballot(todo || rem)) {
-            if (!rem && todo) {
-              const int a = __builtin_ctz(todo);
-              todo &= todo - 1;
-              const uint32_t aat = apw[bl + a], ab = apw[64 + bl + a], al = apw[128 + bl + a];
-              const uint32_t hi = al < n.len ? al : n.len;
-              rem = hi > aat ? hi - aat : 0u;
-              xi = (ab + aat) % A;
-              yi = (n.base + aat) % A;
-              xa = arena_of(S, sgi - k + a);
-              cur = (uint32_t)a;
+          uint32_t found = 0;
+          auto log_match = [&](auto grouping) {
+            constexpr bool G = decltype(grouping)::value;
+            const bool pay = G && pkind == PLAN_PAYLOAD && appended_at >= 0;
+            if constexpr (G) {
+              apw[192 + lane] = ppoff - (uint32_t)appended_at;  // key (payload appends)
+              apw[256 + lane] = pay ? psrc : 0u;               // sender, 0: no payload
             }
-            if (rem) {
-              bool hit;
-              const uint32_t c = log_conflict_chunk<W>(xa, xi, sar, yi, rem, A, hit);
-              if (hit) {
-                found |= 1u << cur;
-                rem = 0;
-              } else {
-                rem -= c;
-                xi += c;
-                yi += c;
-                xi = xi == A ? 0 : xi;
-                yi = yi == A ? 0 : yi;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t todo = active ? apc & ~(1u << k) : 0u;
+            uint32_t cur = 0, rem = 0, xi = 0, yi = 0;
+            const uint2* xa = sar;
+            while (__ballot(todo || rem)) {
+              if (!rem && todo) {
+                const int a = __builtin_ctz(todo);
+                const uint32_t aat = apw[bl + a], ab = apw[64 + bl + a], al = apw[128 + bl + a];
+                uint32_t grp = 1u << a;
+                uint32_t hi = al < n.len ? al : n.len;
+                if constexpr (G) {
+                  const uint32_t akey = apw[192 + bl + a], asrc = apw[256 + bl + a];
+                  if (asrc) {
+  #pragma unroll
+                    for (int s2 = 0; s2 < N; ++s2)
+                      grp |= (uint32_t)(((todo >> s2) & 1) && apw[bl + s2] == aat &&
+                                        apw[128 + bl + s2] == al && apw[192 + bl + s2] == akey &&
+                                        apw[256 + bl + s2] == asrc) << s2;
+                  }
+                  if (asrc && pay && psrc == asrc && ppoff - (uint32_t)appended_at == akey)
+                    hi = min(hi, (uint32_t)appended_at);     // where this lane holds the same copy
+                }
+                todo &= ~grp;
+                rem = hi > aat ? hi - aat : 0u;
+                xi = (ab + aat) % A;
+                yi = (n.base + aat) % A;
+                xa = arena_of(S, sgi - k + a);
+                cur = grp;
+              }
+              if (rem) {
+                bool hit;
+                const uint32_t c = log_conflict_chunk<W>(xa, xi, sar, yi, rem, A, hit);
+                if (hit) {
+                  found |= cur;
+                  rem = 0;
+                } else {
+                  rem -= c;
+                  xi += c;
+                  yi += c;
+                  xi = xi == A ? 0 : xi;
+                  yi = yi == A ? 0 : yi;
+                }
               }
             }
+          };
+          // (N <= 5 kernels run four waves per SIMD at 128 VGPRs: the grouped form costs them
+          // scratch, and their payloads are short)
+          KDevSim* const KG = kargs();
+          if constexpr (N >= 6) {
+            if (KG->dmin == KG->dmax) log_match(std::true_type{});
+            else log_match(std::false_type{});
+          } else {
+            log_match(std::false_type{});
           }
           uint32_t fa = 0;
   #pragma unroll
