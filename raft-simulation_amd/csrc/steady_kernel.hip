@@ -1302,18 +1302,25 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   // request-vote, vote-response and append-entries messages (3F; the responses are in a).
   {
     const uint32_t h = wave_sum(nhb), a = wave_sum(nae), r = wave_sum(nar);
-    const uint32_t ne = wave_sum(el ? 1u : 0u);
     unsigned long long* const ctr =
         S.ctr + (size_t)((blockIdx.x * 4 + wave) % CTR_COPIES) * CTR_STRIDE;
-    if (lane < 9) {
-      const uint32_t msgs = (uint32_t)F * h + a + 3u * F * ne;
+    if (lane < 5) {
+      const uint32_t msgs = (uint32_t)F * h + a;
       const int idx = lane == 0 ? RAFT_CTR_EV_HEARTBEAT : lane == 1 ? RAFT_CTR_EV_AE
-                    : lane == 2 ? RAFT_CTR_EV_AR : lane == 3 ? RAFT_CTR_SENT
-                    : lane == 4 ? RAFT_CTR_DELIVERED : lane == 5 ? RAFT_CTR_EV_TIMEOUT
-                    : lane == 6 ? RAFT_CTR_EV_RV : lane == 7 ? RAFT_CTR_EV_VR : RAFT_CTR_LEADERS;
-      const uint32_t v = lane == 0 ? h : lane == 1 ? a : lane == 2 ? r : lane <= 4 ? msgs
-                       : lane == 5 || lane == 8 ? ne : (uint32_t)F * ne;
+                    : lane == 2 ? RAFT_CTR_EV_AR : lane == 3 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
+      const uint32_t v = lane == 0 ? h : lane == 1 ? a : lane == 2 ? r : msgs;
       if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
+    }
+    if (__builtin_amdgcn_ballot_w64(el)) {                   // wave-uniform
+      const uint32_t ne = wave_sum(el ? 1u : 0u);
+      if (lane < 6) {
+        const int idx = lane == 0 ? RAFT_CTR_EV_TIMEOUT : lane == 1 ? RAFT_CTR_EV_RV
+                      : lane == 2 ? RAFT_CTR_EV_VR : lane == 3 ? RAFT_CTR_LEADERS
+                      : lane == 4 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
+        const uint32_t v = lane == 0 || lane == 3 ? ne : lane <= 2 ? (uint32_t)F * ne
+                                                               : 3u * F * ne;
+        atomicAdd(&ctr[idx], (unsigned long long)v);
+      }
     }
   }
   // ---------------------------------------------------------------- catch-up
