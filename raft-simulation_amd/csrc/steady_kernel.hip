@@ -320,6 +320,7 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
   const uint32_t P = 2 * d + F - 1 + S.hb, allF = (1u << F) - 1;
   uint32_t dl = 0, nhb = 0, nae = 0, nar = 0;  // lines of the block changed; events run
   bool el = false;                             // the cluster's election ran here (general path)
+  uint32_t el_to = 0;                          // its timeouts (two candidates: a tie)
 #ifdef RS_WAVELOG
   uint64_t wl_x1 = 0, wl_x2 = 0, wl_x3 = 0, wl_lend = 0;
 #endif
@@ -502,8 +503,9 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
     // rows end as init-node's (next = mb = 0, match = 0) and nothing is left queued: the script
     // writes the cluster's state after its last event into the registers below, and the cluster is
     // then at the fixed point, which the rest of this path runs to the launch's end (trace hashes,
-    // deadlines and counters as the general body gives them). Anything else -- ties, an election
-    // cut by the launch's end, a state that only looks like init-node -- is bailed as before.
+    // deadlines and counters as the general body gives them). Two timers firing in the same tick
+    // (delay 1) have a script of their own below. Anything else -- near ties, three timers, an
+    // election cut by the launch's end, a state that only looks like init-node -- is bailed.
     {
       auto ifield = [&](int f, int k) { return w[HOT_CW + f * N + k]; };
       bool pat = active && w[0] == 0 && S.Q >= 2u * F && S.el_base >= P && S.hb >= 2 * d + F;
@@ -518,22 +520,30 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
         for (int p = 0; p < 2 * N; ++p) pat = pat && ifield(HF_NEXT + p, k) == 0;
       }
       pat = pat && T != INF;
-      // the candidate: the unique earliest deadline, every other one at least d later
-      uint32_t cidx = 0, t1 = INF;
+      // the candidate: the earliest deadline (the lower index of two equal ones, a tie)
+      uint32_t cidx = 0, t1 = INF, ntie = 0, bidx = 0;
 #pragma unroll
       for (int k = 0; k < N; ++k) {
         const uint32_t dk = ifield(HF_DEADLINE, k);
         cidx = dk < t1 ? (uint32_t)k : cidx;
         t1 = min(t1, dk);
       }
+      bool single = true;
 #pragma unroll
-      for (int k = 0; k < N; ++k)
-        pat = pat && ((uint32_t)k == cidx || (uint64_t)ifield(HF_DEADLINE, k) >= (uint64_t)t1 + d);
+      for (int k = 0; k < N; ++k) {
+        const uint32_t dk = ifield(HF_DEADLINE, k);
+        ntie += dk == t1;
+        bidx = dk == t1 && (uint32_t)k != cidx ? (uint32_t)k : bidx;
+        single = single && ((uint32_t)k == cidx || (uint64_t)dk >= (uint64_t)t1 + d);
+      }
+      // two timers firing together (the delay 1: every other one is then at least d later)
+      const bool tie = ntie == 2 && d == 1 && N >= 3;
       constexpr uint32_t iL = (N + 1) / 2 >= 2 ? (N + 1) / 2 - 2 : 0;   // the electing response
       const uint64_t tL = (uint64_t)t1 + 2 * d + iL;
       const uint64_t tau0 = max((uint64_t)t1 + 2 * d + F, tL + 2 * d);  // the first response
       const uint64_t tlast = tau0 + F - 1;
-      pat = pat && t1 >= t0 && tlast < tend;
+      pat = pat && (single || tie) && t1 >= t0 && (tie || tlast < tend) &&
+            (uint64_t)t1 + 4 * N + 8 < 0xFFFFFFFFull;
       // the election-safety check (P4) compares the new leader's led term with the others'
       // (words past the image: read only when some cluster of the wave qualifies)
       if (__builtin_amdgcn_ballot_w64(pat)) {                 // wave-uniform
@@ -544,9 +554,10 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
 #pragma unroll
         for (int k = 0; k < N; ++k) pat = pat && ((uint32_t)k == cidx || led[k] != T + 1);
       }
-      if (pat) {
+      const uint32_t T1 = T + 1, cid = cidx + 1, peers = ((1u << (N + 1)) - 1) & ~1u & ~(1u << cid);
+      if (pat && single) {
         el = true;
-        const uint32_t T1 = T + 1, cid = cidx + 1;
+        el_to = 1;
         // the candidate's events (node cidx), then each follower's
         uint64_t hc = 0;
 #pragma unroll
@@ -566,7 +577,6 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           hc = trace_event(hc, (uint32_t)tau0 + j, RAFT_MSG_APPEND_RESPONSE, sid, T, RAFT_LEADER,
                            T1, 0);
         }
-        const uint32_t peers = ((1u << (N + 1)) - 1) & ~1u & ~(1u << cid);
 #pragma unroll
         for (int k = 0; k < N; ++k) {
           const bool isc = (uint32_t)k == cidx;
@@ -586,7 +596,124 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
           w[HOT_CW + HF_TRACE_HI * N + k] = (uint32_t)(h >> 32);
         }
         nae = F;                                    // the followers' append-entries and their
-        nar = F;                                    // responses (the rest is counted as nel)
+        nar = F;                                    // responses (the rest is counted as el_to)
+      } else if (pat && tie) {
+        // Two timers at t1 (d = 1): candidates a < b (ids A, B) both time out and send
+        // request-votes; at t1 + 1 every other node grants A's (the lower id's, queued first) and
+        // a and b deny each other (each voted for itself); at t1 + 2 those nodes deny B's. a takes
+        // its vote responses one per tick from t1 + 2 in sender order and is leader at the
+        // majority's one (tL); b takes a's denial at t1 + 2, then the others' from t1 + 3, and
+        // a's append-entries when it arrives at tL + 1 -- when both of b's queues are ready the
+        // alts!! bit of its EVENT draw picks (core.clj:181), and that draw re-arms its timer
+        // exactly. a then takes the responses: the others' at tL + 2 and b's the tick after b
+        // took the append-entries, by (arrival, sender id).
+        const uint32_t a = cidx, b = bidx, B = b + 1;
+        const uint32_t A = cid;
+        constexpr uint32_t M = (N + 1) / 2;                  // majority? (core.clj:19-21)
+        uint64_t ha = 0, hbb = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          const uint64_t h0 = (uint64_t)ifield(HF_TRACE_HI, k) << 32 | ifield(HF_TRACE_LO, k);
+          if ((uint32_t)k == a) ha = h0;
+          if ((uint32_t)k == b) hbb = h0;
+        }
+        ha = trace_event(ha, t1, 6, 0, 0, RAFT_CANDIDATE, T1, 0);
+        ha = trace_event(ha, t1 + 1, RAFT_MSG_REQUEST_VOTE, B, T1, RAFT_CANDIDATE, T1, 0);
+        uint32_t votes = 1, tLt = INF, role = RAFT_CANDIDATE;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {                        // a's vote responses, id order
+          if ((uint32_t)k == a) continue;
+          const uint32_t i = (uint32_t)k - ((uint32_t)k > a ? 1u : 0u), tau = t1 + 2 + i;
+          const bool grant = (uint32_t)k != b;
+          if (grant && role == RAFT_CANDIDATE && ++votes >= M) {
+            role = RAFT_LEADER;
+            tLt = tau;
+          }
+          ha = trace_event(ha, tau, RAFT_MSG_VOTE_RESPONSE, (uint32_t)k + 1, grant ? T : T1, role,
+                           T1, 0);
+        }
+        // b: the denials, then a's append-entries
+        hbb = trace_event(hbb, t1, 6, 0, 0, RAFT_CANDIDATE, T1, 0);
+        hbb = trace_event(hbb, t1 + 1, RAFT_MSG_REQUEST_VOTE, A, T1, RAFT_CANDIDATE, T1, 0);
+        hbb = trace_event(hbb, t1 + 2, RAFT_MSG_VOTE_RESPONSE, A, T1, RAFT_CANDIDATE, T1, 0);
+        uint32_t tb = t1 + 3, j = 0, tbae = INF, brole = RAFT_CANDIDATE, bdl = 0;
+        bool bexact = false;
+        for (int it = 0; it < N + 1; ++it) {
+          const bool res = j < (uint32_t)N - 2, req = tbae == INF;
+          if (!res && !req) break;
+          if (!res && tb < tLt + 1) tb = tLt + 1;             // idle until the append-entries
+          const bool rq = req && tb >= tLt + 1;
+          bool take_req = rq;
+          bexact = false;
+          if (res && rq) {                                    // alts!! (core.clj:181)
+            const uint4 ew = event_draw(g, B, tb, S);
+            take_req = !(ew.x & 1);
+            bexact = true;
+            bdl = tb + S.el_base + __umulhi(ew.y, S.el_span);
+          }
+          if (take_req) {                                     // append-entries-handler 105-123
+            hbb = trace_event(hbb, tb, RAFT_MSG_APPEND_ENTRIES, A, T1, RAFT_FOLLWER, T1, 0);
+            brole = RAFT_FOLLWER;
+            tbae = tb;
+          } else {                                            // the j-th other node's denial
+            uint32_t fid = 0, cnt = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+              const bool other = (uint32_t)k != a && (uint32_t)k != b;
+              fid = other && cnt == j ? (uint32_t)k + 1 : fid;
+              cnt += other;
+            }
+            hbb = trace_event(hbb, tb, RAFT_MSG_VOTE_RESPONSE, fid, T, brole, T1, 0);
+            ++j;
+          }
+          if (!bexact) bdl = tb + S.el_base;                  // + the owed draw
+          ++tb;
+        }
+        const uint32_t tbl = tb - 1;                          // b's last event
+        // a's responses: the others' at tLt + 2, b's at tbae + 1, by (arrival, sender id)
+        uint32_t ta = t1 + N + 1;                             // after its N - 1 vote responses
+        const uint32_t fa = tLt + 2, ba = tbae + 1;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          if ((uint32_t)k == a) continue;
+          const bool isb = (uint32_t)k == b;
+          if (isb && ba != fa) continue;
+          ta = max(ta, fa);
+          ha = trace_event(ha, ta, RAFT_MSG_APPEND_RESPONSE, (uint32_t)k + 1, isb ? T1 : T,
+                           RAFT_LEADER, T1, 0);
+          ++ta;
+        }
+        if (ba != fa) {
+          ta = max(ta, ba);
+          ha = trace_event(ha, ta, RAFT_MSG_APPEND_RESPONSE, B, T1, RAFT_LEADER, T1, 0);
+          ++ta;
+        }
+        const uint32_t tal = ta - 1;                          // a's last event
+        if (tbae != INF && tLt != INF && max(tal, tbl) < tend) {
+          el = true;
+          el_to = 2;
+#pragma unroll
+          for (int k = 0; k < N; ++k) {
+            const bool isa = (uint32_t)k == a, isb = (uint32_t)k == b;
+            uint64_t h = (uint64_t)ifield(HF_TRACE_HI, k) << 32 | ifield(HF_TRACE_LO, k);
+            h = trace_event(h, t1 + 1, RAFT_MSG_REQUEST_VOTE, A, T1, RAFT_FOLLOWER, T, 0);
+            h = trace_event(h, t1 + 2, RAFT_MSG_REQUEST_VOTE, B, T1, RAFT_FOLLOWER, T, 0);
+            h = trace_event(h, tLt + 1, RAFT_MSG_APPEND_ENTRIES, A, T1, RAFT_FOLLWER, T1, 0);
+            h = isa ? ha : isb ? hbb : h;
+            w[HOT_CW + HF_FLAGS * N + k] =
+                isa ? pack_flags(RAFT_LEADER, 0, A, 0, 0, 1)
+                    : pack_flags(RAFT_FOLLWER, 0, A, 0, 0, 0) | (isb && bexact ? 0u : FL_DRAW);
+            w[HOT_CW + HF_MASKS * N + k] = isa ? peers << 16 : 0u;
+            w[HOT_CW + HF_TERM * N + k] = T1;
+            w[HOT_CW + HF_DEADLINE * N + k] = isa ? tal + S.hb : isb ? bdl : tLt + 1 + S.el_base;
+            w[HOT_CW + HF_REQ_TAIL * N + k] = 0;
+            w[HOT_CW + HF_RES_TAIL * N + k] = 0;
+            w[HOT_CW + HF_TRACE_LO * N + k] = (uint32_t)h;
+            w[HOT_CW + HF_TRACE_HI * N + k] = (uint32_t)(h >> 32);
+          }
+          nae = F;
+          nar = F;
+        }
       }
     }
     uint32_t nfl[N], nqm[N];
@@ -1312,13 +1439,15 @@ __global__ void __launch_bounds__(LANE_WG) steady_lane_kernel(DevSim S, uint32_t
       if (v) atomicAdd(&ctr[idx], (unsigned long long)v);
     }
     if (__builtin_amdgcn_ballot_w64(el)) {                   // wave-uniform
-      const uint32_t ne = wave_sum(el ? 1u : 0u);
+      // per election: el_to timeouts, F request-votes and F vote responses per timeout, one
+      // leader, and the request-vote, vote-response and append-entries messages
+      const uint32_t ne = wave_sum(el ? 1u : 0u), nt = wave_sum(el_to);
       if (lane < 6) {
         const int idx = lane == 0 ? RAFT_CTR_EV_TIMEOUT : lane == 1 ? RAFT_CTR_EV_RV
                       : lane == 2 ? RAFT_CTR_EV_VR : lane == 3 ? RAFT_CTR_LEADERS
                       : lane == 4 ? RAFT_CTR_SENT : RAFT_CTR_DELIVERED;
-        const uint32_t v = lane == 0 || lane == 3 ? ne : lane <= 2 ? (uint32_t)F * ne
-                                                               : 3u * F * ne;
+        const uint32_t v = lane == 0 ? nt : lane == 3 ? ne : lane <= 2 ? (uint32_t)F * nt
+                                                                   : (uint32_t)F * (2 * nt + ne);
         atomicAdd(&ctr[idx], (unsigned long long)v);
       }
     }

@@ -145,9 +145,9 @@ def test_gpu_c2_full_size(seed):
     """BASELINE config 2: 65,536 five-node clusters, no faults, for the seeds of SURVEY §8(d) and
     one above 2^32 (Philox key word 1 nonzero): digest-equal after each of four 10k-tick launches.
     The first launch (elections) runs the steady kernel, which runs init-node's election in closed
-    form and hands the clusters it cannot (two timers within d of each other: under 0.2 %) to the
-    general body; the last one is the steady kernel alone on the 256-workgroup grid with no cluster
-    bailed (core.clj:91-139,105-123,141-149,162-169)."""
+    form, two timers firing together included (about 30 clusters per seed; only three together
+    would be handed to the general body); the last one is the steady kernel alone on the
+    256-workgroup grid with no cluster bailed (core.clj:91-139,105-123,141-149,162-169,181)."""
     cfg = dict(n_clusters=65536, nodes=5, seed=seed)
     g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
     helpers.oracle_threads(r, helpers.cpu_threads())
@@ -159,7 +159,7 @@ def test_gpu_c2_full_size(seed):
         bad = np.nonzero(g.digest() != r.digest())[0]
         assert not len(bad), f"launch {launch}: {len(bad)} clusters differ, first {bad[0]}"
     assert g.counters() == r.counters()
-    assert 0 <= bails[0] < 65536 // 500 and bails[-1] == 0, bails
+    assert 0 <= bails[0] <= 2 and bails[-1] == 0, bails
 
 
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
@@ -445,7 +445,7 @@ def test_gpu_steady_path_taken():
         bails.append(g.diag_last_bails())
         assert (g.digest() == r.digest()).all()
     assert g.counters() == r.counters()
-    assert 0 <= bails[0] < 65536 // 500 and bails[-1] == 0, bails
+    assert 0 <= bails[0] <= 2 and bails[-1] == 0, bails
 
 
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
