@@ -11,7 +11,7 @@
 
 namespace rs {
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
-                       hipEvent_t ev1, bool steady);
+                       hipEvent_t ev1, bool steady, bool storm);
 hipError_t launch_sched_key(const DevSim& S, uint32_t t0, hipStream_t st);
 hipError_t launch_sched_perm(const DevSim& S, uint32_t* zero, uint32_t* perm, uint32_t* nslots,
                              hipStream_t st);
@@ -87,6 +87,10 @@ struct Shard {
   int steady_mode;                     // 0 auto, 1 always, 2 never
   uint32_t* bail_host;                 // host-mapped word (hipHostMalloc)
   uint32_t steady_cooldown;
+  // Ticks before this one are storm ticks (tick_wave.hpp, STORM): the handle is fresh from
+  // init-node with client traffic, so no timer fires before el_base and the only events are
+  // client-sets at followers. Any host write of state or of the clock ends it (0).
+  uint32_t storm_until;
 };
 constexpr uint32_t STEADY_COOLDOWN = 2;
 // The wave packing is rebuilt every RESORT_EVERY-th tick launch and reused in between: with
@@ -238,6 +242,9 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   }
 #endif
   s->steady_ok = d.lite && s->N <= 5 && !d.TC && !(cfg->variant_flags & RAFT_VARIANT_SPEC);
+  // init-node's deadlines are el_base or more ahead and every re-arm is too (SIM_SPEC D4; the
+  // Spec-Raft control re-arms on fewer events): until el_base, client-sets are the only events
+  s->storm_until = cfg->client_ppm && !d.TC ? cfg->el_base : 0u;
   s->resort_every = d.lite ? RESORT_EVERY_LITE : RESORT_EVERY;
   {
     const char* le = getenv("RAFTSIM_LAUNCH_EVENTS");
@@ -309,8 +316,11 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     s->pending = true;
   }
   for (uint32_t done = 0; done < n_ticks;) {
-    const uint32_t nt = std::min(s->tpl, n_ticks - done);
+    uint32_t nt = std::min(s->tpl, n_ticks - done);
     const uint32_t t0 = (uint32_t)s->tick;
+    // storm ticks run alone in a launch of their own (the STORM body)
+    const bool storm = t0 < s->storm_until;
+    if (storm) nt = std::min(nt, s->storm_until - t0);
     // Path (speed only: both paths give the same state). Host writes may have cleared lite.
     bool steady = s->steady_ok && s->d.lite;
     if (steady && s->steady_mode == 2) steady = false;
@@ -384,7 +394,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     if (no_keys) D.shist = nullptr;
     HIP_OK(rs::launch_tick(D, t0, nt, s->stream,
                            timed ? s->kev[2 * launches] : nullptr,
-                           timed ? s->kev[2 * launches + 1] : nullptr, steady));
+                           timed ? s->kev[2 * launches + 1] : nullptr, steady, storm && !steady));
     done += nt;
     s->tick += nt;
     s->ticks_run += nt;
@@ -503,6 +513,7 @@ static int sh_read_nodes(Shard* s, uint32_t c0, uint32_t nc, raft_node_t* out) {
 static int sh_write_nodes(Shard* s, uint32_t c0, uint32_t nc, const raft_node_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
+  s->storm_until = 0;
   if (!in) return fail(-EINVAL, "null input");
   HIP_OK(hipSetDevice(s->cfg.device));
   const uint32_t N = s->N, all = ((1u << (N + 1)) - 1) & ~1u;
@@ -572,6 +583,7 @@ static int sh_read_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which
 static int sh_write_queue(Shard* s, uint32_t cluster, uint32_t id, uint32_t which,
                          const raft_msg_t* in, uint32_t count) {
   int rc = check_node(s, cluster, id);
+  if (!rc) s->storm_until = 0;
   if (rc) return rc;
   if (which > 1 || count > s->Q || (count && !in)) return fail(-EINVAL, "bad queue or count");
   for (uint32_t i = 0; i < count; ++i) {
@@ -625,6 +637,7 @@ static int sh_read_arena(Shard* s, uint32_t cluster, uint32_t id, raft_entry_t* 
 static int sh_write_arena(Shard* s, uint32_t cluster, uint32_t id, const raft_entry_t* in,
                          uint32_t count) {
   int rc = check_node(s, cluster, id);
+  if (!rc) s->storm_until = 0;
   if (rc) return rc;
   if (count > s->A || (count && !in)) return fail(-EINVAL, "count > arena_cap");
   HIP_OK(hipSetDevice(s->cfg.device));
@@ -658,6 +671,7 @@ static int sh_read_commit_stream(Shard* s, uint32_t cluster, uint32_t id, uint32
 static int sh_write_commit_stream(Shard* s, uint32_t cluster, uint32_t id, const uint32_t* in,
                                  uint32_t count) {
   int rc = check_node(s, cluster, id);
+  if (!rc) s->storm_until = 0;
   if (rc) return rc;
   HIP_OK(hipSetDevice(s->cfg.device));
   const uint32_t SC = s->cfg.commit_stream_cap;
@@ -738,6 +752,7 @@ static int sh_read_clusters(Shard* s, uint32_t c0, uint32_t nc, raft_cluster_t* 
 static int sh_write_clusters(Shard* s, uint32_t c0, uint32_t nc, const raft_cluster_t* in) {
   int rc = check_range(s, c0, nc);
   if (rc) return rc;
+  s->storm_until = 0;
   HIP_OK(hipSetDevice(s->cfg.device));
   std::vector<raft_cluster_t> buf(in, in + nc);
   for (auto& h : buf) {
@@ -894,6 +909,7 @@ int raft_sim_set_tick(raft_sim_t* r, uint64_t tick) {
     const int rc = sh_sync(s);
     if (rc) return rc;
     s->tick = tick;
+    s->storm_until = 0;
     // the packing keys are relative to the next launch's first tick: the next rebuild computes
     // them from the state
     s->keys_written = false;

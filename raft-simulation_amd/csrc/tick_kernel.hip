@@ -12,12 +12,13 @@ namespace rs {
 // 4-wave workgroups 1-2 % slower on C2/C3/C4). The grid covers the packing's slot bound. The
 // compiler is asked for 4 waves per SIMD (<= 128 VGPRs) where it meets that without spilling:
 // N <= 5, and the faithful kernels up to N = 6 (N = 7, 8 would spill).
-template <int N, bool TRACE, bool SPEC, bool LITE>
+template <int N, bool TRACE, bool SPEC, bool LITE, bool STORM = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(!TRACE && (N <= 5 || (!SPEC && N <= 6)) ? 4 : 1, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  tick_wave<N, TRACE, SPEC, LITE>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x, gridDim.x, S.perm,
-                                  S.perm ? *S.nslots : S.C, nullptr, blockIdx.x);
+  tick_wave<N, TRACE, SPEC, LITE, false, STORM>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x,
+                                                gridDim.x, S.perm, S.perm ? *S.nslots : S.C,
+                                                nullptr, blockIdx.x);
 }
 
 // RAFT_SCHED_ALIGNED wave packing: a counting sort of the clusters by their next event tick
@@ -310,7 +311,7 @@ hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t 
 
 template <int N, bool SPEC>
 hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
-                    hipEvent_t ev1, bool steady) {
+                    hipEvent_t ev1, bool steady, bool storm) {
   constexpr int CPW = 64 / N;
   constexpr size_t lds = block_lds_bytes<N, SPEC>();
   const uint32_t waves = S.perm ? sched_slots_bound(S.C, N) / CPW : (S.C + CPW - 1) / CPW;
@@ -318,7 +319,10 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
     // the steady kernel, whose workgroups run the clusters they bail through tick_wave
     if (steady) return launch_steady(S, t0, nt, st, ev0, ev1);
   }
-  if (S.TC)
+  if (storm && !S.TC && !S.lite)
+    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false, true>), dim3(waves), dim3(64), lds,
+                          st, ev0, ev1, 0, S, t0, nt);
+  else if (S.TC)
     hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC, false>), dim3(waves), dim3(64), lds, st, ev0,
                           ev1, 0, S, t0, nt);
   else if (!SPEC && S.lite)
@@ -332,31 +336,33 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
 
 template <int N>
 hipError_t launch_tick_n(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
-                         hipEvent_t ev0, hipEvent_t ev1, bool steady) {
-  if (S.variant & RAFT_VARIANT_SPEC) return launch_tick_ns<N, true>(S, t0, nt, st, ev0, ev1, false);
-  return launch_tick_ns<N, false>(S, t0, nt, st, ev0, ev1, steady);
+                         hipEvent_t ev0, hipEvent_t ev1, bool steady, bool storm) {
+  if (S.variant & RAFT_VARIANT_SPEC)
+    return launch_tick_ns<N, true>(S, t0, nt, st, ev0, ev1, false, storm);
+  return launch_tick_ns<N, false>(S, t0, nt, st, ev0, ev1, steady, storm);
 }
 
-// steady: a LITE launch at N <= 5 without TRACE runs the steady kernel (the caller decides;
-// results are the same either way)
+// steady: a LITE launch at N <= 5 without TRACE runs the steady kernel; storm: a launch before any
+// timer can fire in a handle fresh from init-node runs the STORM body (tick_wave.hpp). The caller
+// decides; results are the same either way.
 hipError_t launch_tick(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
-                       hipEvent_t ev1, bool steady) {
+                       hipEvent_t ev1, bool steady, bool storm) {
   switch (S.N) {
-    case 2: return launch_tick_n<2>(S, t0, nt, st, ev0, ev1, steady);
-    case 3: return launch_tick_n<3>(S, t0, nt, st, ev0, ev1, steady);
-    case 4: return launch_tick_n<4>(S, t0, nt, st, ev0, ev1, steady);
-    case 5: return launch_tick_n<5>(S, t0, nt, st, ev0, ev1, steady);
-    case 6: return launch_tick_n<6>(S, t0, nt, st, ev0, ev1, false);
-    case 7: return launch_tick_n<7>(S, t0, nt, st, ev0, ev1, false);
-    case 8: return launch_tick_n<8>(S, t0, nt, st, ev0, ev1, false);
-    case 9: return launch_tick_n<9>(S, t0, nt, st, ev0, ev1, false);
+    case 2: return launch_tick_n<2>(S, t0, nt, st, ev0, ev1, steady, storm);
+    case 3: return launch_tick_n<3>(S, t0, nt, st, ev0, ev1, steady, storm);
+    case 4: return launch_tick_n<4>(S, t0, nt, st, ev0, ev1, steady, storm);
+    case 5: return launch_tick_n<5>(S, t0, nt, st, ev0, ev1, steady, storm);
+    case 6: return launch_tick_n<6>(S, t0, nt, st, ev0, ev1, false, storm);
+    case 7: return launch_tick_n<7>(S, t0, nt, st, ev0, ev1, false, storm);
+    case 8: return launch_tick_n<8>(S, t0, nt, st, ev0, ev1, false, storm);
+    case 9: return launch_tick_n<9>(S, t0, nt, st, ev0, ev1, false, storm);
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int N, bool TRACE, bool SPEC, bool LITE = false>
+template <int N, bool TRACE, bool SPEC, bool LITE = false, bool STORM = false>
 hipError_t configure_one() {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC, LITE>),
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC, LITE, STORM>),
                              hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)block_lds_bytes<N, SPEC>());
 }
@@ -366,7 +372,9 @@ hipError_t configure_n() {
   hipError_t e = hipSuccess;
   if ((e = configure_one<N, false, false>()) || (e = configure_one<N, true, false>()) ||
       (e = configure_one<N, false, true>()) || (e = configure_one<N, true, true>()) ||
-      (e = configure_one<N, false, false, true>()))
+      (e = configure_one<N, false, false, true>()) ||
+      (e = configure_one<N, false, false, false, true>()) ||
+      (e = configure_one<N, false, true, false, true>()))
     return e;
   return hipSuccess;
 }

@@ -433,18 +433,26 @@ __device__ __forceinline__ uint32_t sched_key_of(uint32_t deadline, const QueueR
 // fault-free delivery pack, and P3/P4 copy and compare one entry per memory round trip (they only
 // see host-written logs there). The compiler then drops that code: 121 -> ~100 VGPRs at N = 5.
 //
+// STORM: the launch lies before any timer can fire in a handle fresh from init-node (ticks
+// [0, el_base): init-node's deadlines and every re-arm are el_base or more ahead), so no node is
+// or becomes a candidate or a leader and no network message exists: the only events are
+// client-sets at followers, which redirect (SIM_SPEC D15; redirects are outside the fault model).
+// The host picks it (raftsim.hip, storm_until); the compiler drops the other handlers, the
+// emission and fault draws, P3, P4 and the drain.
+//
 // tick_wave runs one wave's clusters: `smem` is the wave's LDS (block_lds_bytes), `lane` its lane,
 // and the wave takes wave slots wave0, wave0 + wstride, ... below nslots; slot s holds clusters
 // perm[s * CPW ...] (null perm: the identity). CATCH: each cluster resumes at resume[slot] (the
 // tick the steady kernel stopped it before) instead of t0. The wave's counters go to copy
 // ctr_copy (mod CTR_COPIES) of the counter block.
-template <int N, bool TRACE, bool SPEC, bool LITE, bool CATCH = false>
+template <int N, bool TRACE, bool SPEC, bool LITE, bool CATCH = false, bool STORM = false>
 __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t nt, uint32_t* smem,
                                           int lane, uint32_t wave0, uint32_t wstride,
                                           const uint32_t* perm, uint32_t nslots,
                                           const uint32_t* resume, uint32_t ctr_copy) {
   static_assert(!LITE || (!TRACE && !SPEC), "LITE is the plain faithful kernel");
   static_assert(!CATCH || LITE, "catch-up launches follow the steady kernel (LITE only)");
+  static_assert(!STORM || (!LITE && !TRACE && !CATCH), "STORM: client traffic, no trace rings");
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
@@ -535,7 +543,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // cluster's (count + l)-th injection, an inclusive scan of (1 + gap) over the lanes gives the
     // next 64 injections' on-tick numbers, and the first one at or past tend ends the cluster's
     // run (SIM_SPEC P0; the Spec-Raft control's client-sets reach halted nodes the same way).
-    if constexpr (!LITE) {
+    if constexpr (!LITE && !STORM) {
       const bool dead = ((uint32_t)(__ballot(active && n.fault) >> bl0) & cmask) == cmask;
       if (kargs()->client_ppm && !__ballot(active && !dead) && __ballot(active && cnext < tend)) {
         const uint64_t heads = __ballot(active && k0 == 0);
@@ -778,7 +786,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // The next timeout of a non-leader (core.clj:174) takes the tick's draw when there is one,
       // else its draw is deferred (leaders' events need none).
       uint4 w = make_uint4(0, 0, 0, 0);
-      const bool tdraw = !SPEC && live && dpend[lane] && !req_ok && !res_ok && n.deadline <= t;
+      const bool tdraw = !SPEC && !STORM && live && dpend[lane] && !req_ok && !res_ok &&
+                         n.deadline <= t;
       bool have_w = (req_ok && res_ok) ||
                     (!LITE && req_ok && n.role != RAFT_LEADER && n.lid == 0);
       if (have_w || tdraw) {
@@ -865,7 +874,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         const bool was_leader = n.role == RAFT_LEADER;
         bool rearm = false;           // SPEC: the event resets the election timer (SIM_SPEC §8)
 
-        if constexpr (SPEC) {
+        if constexpr (STORM) {
+          ev = type;                  // a client-set at a follower: redirect-client (below)
+          emit = 4;
+        } else if constexpr (SPEC) {
           spec_handle<N, MAJ>(S, n, lsw, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
                               emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
                               pold_base, preloc, papplied, elected, mchg, rearm);
@@ -1116,7 +1128,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // ------------------------------------------------ emission (rpc / respond)
           // The message words go to the pair cells, then each message's fault draws (its delivery
           // pack, in the cell's last word) and the receiver's bit into sentmask.
-          if (emit) {
+          if (!STORM && emit) {
             // the cluster's partition draw for this tick's epoch, made once per epoch (SIM_SPEC P2)
             uint32_t pstate = 0;
             if (!LITE && kargs()->part_ppm) {
@@ -1256,7 +1268,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // m entries were added at position n.len - m (appended_at, -1 when none)
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
       const int appended_at = m ? (int)(n.len - m) : -1;
-      if (__ballot(m || papplied || (TRACE && tr_cnt))) {
+      if (!STORM && __ballot(m || papplied || (TRACE && tr_cnt))) {
         const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
         if (m) {
           const uint32_t pold_len = n.len - m;
@@ -1314,7 +1326,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // ---------------------------------------------------------------- P4 invariant checker
       // the majority-match scan can raise hwm only when the leader's log reaches past it
       const bool mcheck = (elected || mchg) && n.len > hidx;
-      if (__ballot(elected || appended_at >= 0 || mcheck)) {
+      if (!STORM && __ballot(elected || appended_at >= 0 || mcheck)) {
         if (__ballot(elected)) {                       // election safety
           bool bad = false;
   #pragma unroll
@@ -1486,7 +1498,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // traffic a cluster has an event nearly every tick of a burst: measured C3 +3 % with one
       // wave-wide clock, unchanged with per-cluster clocks, C4-N9 +1 %), and it would cost the
       // larger-N kernels occupancy (N = 9: 125 -> 129 VGPRs).
-      if constexpr (!SPEC && !TRACE && N <= 5) if (LITE || !kargs()->client_ppm) {
+      if constexpr (!SPEC && !TRACE && !STORM && N <= 5) if (LITE || !kargs()->client_ppm) {
         // leaders whose responses can drain: a log past the hwm makes a success response a
         // checker event (C3/C4 replication), so those leaders stay with the loop
         const bool elig = on && !n.fault && n.role == RAFT_LEADER && n.len <= hidx;

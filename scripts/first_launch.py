@@ -15,5 +15,7 @@ wl, C, K, lib = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
 sim = Backend(lib, "raft_sim_", n_clusters=C, **bench.WORKLOADS[wl]["cfg"])
 for _ in range(K):
     sim.step(10000)
-    print(f"{wl} launch ms {sim.last_step_timing()[0]:.3f}", flush=True)
+    ms, nl = sim.last_step_timing()
+    print(f"{wl} launch ms {sim.last_span():.3f} (step span; {nl} launches, avg {ms:.3f})",
+          flush=True)
 sim.close()
