@@ -13,7 +13,7 @@ namespace rs {
 // compiler is asked for 4 waves per SIMD (<= 128 VGPRs) where it meets that without spilling:
 // N <= 5, and the faithful kernels up to N = 6 (N = 7, 8 would spill).
 template <int N, bool TRACE, bool SPEC, bool LITE, bool STORM = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(!TRACE && (N <= 5 || (!SPEC && N <= 6)) ? 4 : 1, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STORM && N <= 5 ? 5 : !TRACE && (N <= 5 || (!SPEC && N <= 6)) ? 4 : 1, 8)))
 tick_kernel(DevSim S, uint32_t t0, uint32_t nt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   tick_wave<N, TRACE, SPEC, LITE, false, STORM>(S, t0, nt, smem, (int)threadIdx.x, blockIdx.x,
@@ -320,8 +320,8 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
     if (steady) return launch_steady(S, t0, nt, st, ev0, ev1);
   }
   if (storm && !S.TC && !S.lite)
-    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false, true>), dim3(waves), dim3(64), lds,
-                          st, ev0, ev1, 0, S, t0, nt);
+    hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false, true>), dim3(waves), dim3(64),
+                          block_lds_bytes<N, SPEC, true>(), st, ev0, ev1, 0, S, t0, nt);
   else if (S.TC)
     hipExtLaunchKernelGGL((tick_kernel<N, true, SPEC, false>), dim3(waves), dim3(64), lds, st, ev0,
                           ev1, 0, S, t0, nt);
@@ -364,7 +364,7 @@ template <int N, bool TRACE, bool SPEC, bool LITE = false, bool STORM = false>
 hipError_t configure_one() {
   return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel<N, TRACE, SPEC, LITE, STORM>),
                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)block_lds_bytes<N, SPEC>());
+                             (int)block_lds_bytes<N, SPEC, STORM>());
 }
 
 template <int N>

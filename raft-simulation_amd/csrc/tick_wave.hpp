@@ -407,14 +407,18 @@ template <int N>
 constexpr int part_words() { return 2 * (64 / N); }
 template <int N>
 constexpr int cq_words() { return 64 + 64 + 16 + 64 / N; }
-template <int N, bool SPEC>
+// (the STORM body has no leader, whose rows NM_LDS would hold: its waves take 2.5 KB less at N = 5,
+// five per SIMD instead of four)
+template <int N, bool STORM = false>
+constexpr bool nm_lds_in() { return nm_lds<N>() && !STORM; }
+template <int N, bool SPEC, bool STORM = false>
 constexpr int wave_lds_words() {
-  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds<N>() ? 2 * N * 64 : 0) +
+  return cell_words<N>() + LCTR_WORDS + (SPEC ? 64 : 0) + (nm_lds_in<N, STORM>() ? 2 * N * 64 : 0) +
          trip_words<N>() + DPEND_WORDS + part_words<N>() + cq_words<N>();
 }
-template <int N, bool SPEC>
+template <int N, bool SPEC, bool STORM = false>
 constexpr size_t block_lds_bytes() {
-  return wave_lds_words<N, SPEC>() * sizeof(uint32_t);
+  return wave_lds_words<N, SPEC, STORM>() * sizeof(uint32_t);
 }
 // N <= 5 kernels run four waves per SIMD: sixteen one-wave blocks must fit the CU's 160 KB
 static_assert(block_lds_bytes<5, true>() * 16 <= 160 * 1024, "N = 5 LDS budget");
@@ -463,7 +467,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   int32_t* nmL = reinterpret_cast<int32_t*>(fr + (SPEC ? 64 : 0));   // NM_LDS rows
   if (lane < LCTR_WORDS) lctr[lane] = lane == LCTR_FIRSTVIOL ? INF : 0u;
   // in LDS: one more loop-carried VGPR cost C3's kernel a wave per SIMD
-  uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds<N>() ? 2 * N * 64 : 0);
+  uint32_t* tripsL = reinterpret_cast<uint32_t*>(nmL) + (nm_lds_in<N, STORM>() ? 2 * N * 64 : 0);
   uint32_t* const dpend = tripsL + trip_words<N>();      // (likewise)
   dpend[lane] = 0;
   uint32_t* const pcache = dpend + DPEND_WORDS;    // [CPW] epochs, then [CPW] draws
@@ -512,7 +516,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       n.base = hp[hf_abase(N) * N]; n.front = hp[hf_afront(N) * N]; n.led = hp[hf_led(N) * N];
       n.trace = (uint64_t)hp[HF_TRACE_HI * N] << 32 | hp[HF_TRACE_LO * N];
       hidx = hc[0]; hterm = hc[1]; hval = hc[2]; cnext = hc[3]; ccount = hc[4];
-      if constexpr (nm_lds<N>()) {     // each lane only ever touches its own LDS column
+      if constexpr (nm_lds_in<N, STORM>()) {   // each lane only touches its own LDS column
   #pragma unroll
         for (int p = 0; p < N; ++p) {
           nmL[p * 64 + lane] = hp[(HF_NEXT + p) * N];
@@ -716,7 +720,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       uint32_t* const mysrec = cells + pair_words<N>() + bl * SRECW;
       uint2* const sar = arena_of(S, sgi);
       int32_t* const hnm = reinterpret_cast<int32_t*>(S.hot + (size_t)(sg - S.goff) * HB + HOT_CW + k);
-      const PeerW lsw = nm_lds<N>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
+      const PeerW lsw = nm_lds_in<N, STORM>() ? PeerW{nmL + lane, nmL + N * 64 + lane, 64u}
                                    : PeerW{hnm + HF_NEXT * N, hnm + (HF_NEXT + N) * N, (uint32_t)N};
       if constexpr (SPEC) {          // payloads are judged against the senders' pre-tick frontiers
         fr[lane] = n.front;
@@ -1690,7 +1694,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       hp[HF_REQ_TAIL * N] = n.rq.tail; hp[HF_RES_TAIL * N] = n.rs.tail;
       hp[hf_abase(N) * N] = n.base; hp[hf_afront(N) * N] = n.front; hp[hf_led(N) * N] = n.led;
       hp[HF_TRACE_LO * N] = (uint32_t)n.trace; hp[HF_TRACE_HI * N] = (uint32_t)(n.trace >> 32);
-      if constexpr (nm_lds<N>()) {
+      if constexpr (nm_lds_in<N, STORM>()) {
   #pragma unroll
         for (int p = 0; p < N; ++p) {
           hp[(HF_NEXT + p) * N] = nmL[p * 64 + lane];
