@@ -162,6 +162,40 @@ def test_gpu_c2_full_size(seed):
     assert 0 <= bails[0] <= 2 and bails[-1] == 0, bails
 
 
+@pytest.mark.parametrize("variant,nodes", [(0, 5), (2, 5), (3, 5), (0, 9), (2, 7)])
+def test_gpu_storm_window(variant, nodes):
+    """The STORM body (tick_wave.hpp): a fresh handle with client traffic runs the ticks before
+    el_base -- where only client-sets at followers and their redirects can happen -- as a launch of
+    its own, split off the first step; digest- and counter-equal to the oracle after it and after
+    the elections that follow (core.clj:151-160 with server.clj:62-63; 166-169). A host write of the
+    clock ends the storm ticks: the same step is then one launch, with the same results."""
+    cfg = dict(n_clusters=4096, nodes=nodes, seed=11 + variant, hb=400, el_base=1500, el_span=800,
+               client_ppm=300000, client_period=4096, client_burst=1024, client_redirects=4,
+               log_cap=256, variant_flags=variant, drop_ppm=50000, dmin=1, dmax=20)
+    r = helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    g = helpers.gpu(ticks_per_launch=4000, **cfg)
+    g.step(4000)
+    r.step(4000)
+    assert g.last_step_timing()[1] == 2                  # [0, 1500) storm, then [1500, 4000)
+    assert np.array_equal(g.digest(), r.digest())
+    g.step(4000)
+    r.step(4000)
+    assert g.last_step_timing()[1] == 1
+    assert np.array_equal(g.digest(), r.digest())
+    c = g.counters()
+    assert c == r.counters() and c["redirects"] > 0 and c["leaders"] > 0
+    g.close()
+    g2 = helpers.gpu(ticks_per_launch=4000, **cfg)
+    g2.set_tick(0)                                       # a host write of the clock
+    g2.step(4000)
+    assert g2.last_step_timing()[1] == 1
+    r2 = helpers.oracle(**cfg)
+    helpers.oracle_threads(r2, helpers.cpu_threads())
+    r2.step(4000)
+    assert np.array_equal(g2.digest(), r2.digest())
+
+
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
 def test_gpu_init_election_closed_form(nodes, d):
     """The steady kernel's election from init-node (steady_kernel.hip) for every follower count
@@ -446,6 +480,40 @@ def test_gpu_steady_path_taken():
         assert (g.digest() == r.digest()).all()
     assert g.counters() == r.counters()
     assert 0 <= bails[0] <= 2 and bails[-1] == 0, bails
+
+
+@pytest.mark.parametrize("variant,nodes", [(0, 5), (2, 5), (3, 5), (0, 9), (2, 7)])
+def test_gpu_storm_window(variant, nodes):
+    """The STORM body (tick_wave.hpp): a fresh handle with client traffic runs the ticks before
+    el_base -- where only client-sets at followers and their redirects can happen -- as a launch of
+    its own, split off the first step; digest- and counter-equal to the oracle after it and after
+    the elections that follow (core.clj:151-160 with server.clj:62-63; 166-169). A host write of the
+    clock ends the storm ticks: the same step is then one launch, with the same results."""
+    cfg = dict(n_clusters=4096, nodes=nodes, seed=11 + variant, hb=400, el_base=1500, el_span=800,
+               client_ppm=300000, client_period=4096, client_burst=1024, client_redirects=4,
+               log_cap=256, variant_flags=variant, drop_ppm=50000, dmin=1, dmax=20)
+    r = helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    g = helpers.gpu(ticks_per_launch=4000, **cfg)
+    g.step(4000)
+    r.step(4000)
+    assert g.last_step_timing()[1] == 2                  # [0, 1500) storm, then [1500, 4000)
+    assert np.array_equal(g.digest(), r.digest())
+    g.step(4000)
+    r.step(4000)
+    assert g.last_step_timing()[1] == 1
+    assert np.array_equal(g.digest(), r.digest())
+    c = g.counters()
+    assert c == r.counters() and c["redirects"] > 0 and c["leaders"] > 0
+    g.close()
+    g2 = helpers.gpu(ticks_per_launch=4000, **cfg)
+    g2.set_tick(0)                                       # a host write of the clock
+    g2.step(4000)
+    assert g2.last_step_timing()[1] == 1
+    r2 = helpers.oracle(**cfg)
+    helpers.oracle_threads(r2, helpers.cpu_threads())
+    r2.step(4000)
+    assert np.array_equal(g2.digest(), r2.digest())
 
 
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
