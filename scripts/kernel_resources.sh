@@ -21,10 +21,10 @@ for m in re.finditer(r'^(_ZN2rs\w+):\s', s, re.M):
     tail = s[s.index('.Lfunc_end', m.end()):][:4000]
     get = lambda k: (re.search(r'; ' + k + r': (\d+)', tail) or [None, '?'])[1]
     pretty = name.replace('_ZN2rs', 'rs::')
-    mt = re.match(r'rs::11tick_kernelILi(\d)ELb(\d)ELb(\d)ELb(\d)', pretty)
+    mt = re.match(r'rs::11tick_kernelILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)', pretty)
     if mt:
         pretty = (f"tick_kernel<N={mt.group(1)}, TRACE={mt.group(2)}, SPEC={mt.group(3)}, "
-                  f"LITE={mt.group(4)}>")
+                  f"LITE={mt.group(4)}{', STORM' if mt.group(5) == '1' else ''}>")
     ml = re.match(r'rs::18steady_lane_kernelILi(\d)E', pretty)
     if ml:
         pretty = f"steady_lane_kernel<N={ml.group(1)}>"
