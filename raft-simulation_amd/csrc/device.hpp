@@ -93,6 +93,10 @@ struct DevSim {
   uint32_t* nbail_zero;     // the previous steady launch's word (two alternate): reported to
                             // bail_report and zeroed by this launch
   uint32_t* bail_report;    // host-mapped word (the host picks the next launches' path from it)
+  // Storm launches (storm_kernel.hip): the clusters the lane-per-cluster kernel leaves to the
+  // general STORM body, and their number (device word)
+  uint32_t* storm_list;
+  uint32_t* storm_count;
 };
 
 // The kernel's DevSim argument, read where a field is used. The kernels that run the tick body
@@ -354,6 +358,17 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
   x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x118, 0xf, 0xf, false));
   x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x142, 0xa, 0xf, false));
   x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)INF, (int)x, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
+// Wave-wide sum (all 64 lanes active), uniform: DPP row shifts and broadcasts as in wave_min.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return __builtin_amdgcn_readlane(x, 63);
 }
 

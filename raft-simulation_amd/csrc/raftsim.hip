@@ -254,6 +254,17 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
     sh_destroy(s);
     return rc;
   }
+  // the storm kernel's leftover list (storm_kernel.hip), while storm ticks lie ahead. One lane per
+  // cluster needs clusters enough to fill the chip (two 64-cluster waves per SIMD at least: at
+  // C4's 16,384 clusters its 256 waves ran 36 ms against the lane-per-node body's 14): below that
+  // the storm ticks run the general STORM body.
+  // (Its registers hold arrivals below 2^28 and hop counts below 16.)
+  if (s->storm_until && s->C >= 131072 && cfg->el_base < (1u << 28) && cfg->client_redirects < 16 &&
+      ((rc = dalloc(s, &s->d.storm_list, s->C)) ||
+                         (rc = dalloc(s, &s->d.storm_count, 1)))) {
+    sh_destroy(s);
+    return rc;
+  }
   if (s->steady_ok) {
     const char* m = getenv("RAFTSIM_STEADY");
     s->steady_mode = m && !strcmp(m, "always") ? 1 : m && !strcmp(m, "never") ? 2 : 0;

@@ -95,17 +95,6 @@ __host__ __device__ constexpr uint64_t trace_geo() {
   return s;
 }
 
-// Wave-wide sum (all 64 lanes active), uniform: DPP row shifts and broadcasts as in wave_min.
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-  return __builtin_amdgcn_readlane(x, 63);
-}
-
 // A cluster at its fixed point, lane-resident: every follower took the leader's append-entries
 // (flags, votes, term and commit are what another one sets again), every response succeeded (next /
 // match / keys as another one sets them), the log is empty (a heartbeat ships nothing). With the

@@ -309,6 +309,33 @@ __global__ void digest_kernel(DevSim S, uint32_t c0, uint32_t nc, unsigned long 
 hipError_t launch_steady(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
                          hipEvent_t ev0, hipEvent_t ev1);
 
+hipError_t launch_storm(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
+                        hipEvent_t ev1);
+
+// The general STORM body over the clusters S.perm lists (S.nslots of them: the storm kernel's
+// leftovers): one wave slot per listed cluster at most, waves past the list exit at once.
+template <int N, bool SPEC>
+hipError_t launch_storm_body_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
+                                hipEvent_t ev0, hipEvent_t ev1) {
+  constexpr int CPW = 64 / N;
+  hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false, true>), dim3((S.C + CPW - 1) / CPW),
+                        dim3(64), block_lds_bytes<N, SPEC, true>(), st, ev0, ev1, 0, S, t0, nt);
+  return hipGetLastError();
+}
+hipError_t launch_storm_body(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st,
+                             hipEvent_t ev0, hipEvent_t ev1) {
+  const bool spec = S.variant & RAFT_VARIANT_SPEC;
+  switch (S.N) {
+#define RS_SB(NN)                                                                            \
+  case NN:                                                                                   \
+    return spec ? launch_storm_body_ns<NN, true>(S, t0, nt, st, ev0, ev1)                    \
+                : launch_storm_body_ns<NN, false>(S, t0, nt, st, ev0, ev1);
+    RS_SB(2) RS_SB(3) RS_SB(4) RS_SB(5) RS_SB(6) RS_SB(7) RS_SB(8) RS_SB(9)
+#undef RS_SB
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int N, bool SPEC>
 hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t st, hipEvent_t ev0,
                     hipEvent_t ev1, bool steady, bool storm) {
@@ -319,6 +346,8 @@ hipError_t launch_tick_ns(const DevSim& S, uint32_t t0, uint32_t nt, hipStream_t
     // the steady kernel, whose workgroups run the clusters they bail through tick_wave
     if (steady) return launch_steady(S, t0, nt, st, ev0, ev1);
   }
+  if (storm && !S.TC && !S.lite && S.storm_list)
+    return launch_storm(S, t0, nt, st, ev0, ev1);
   if (storm && !S.TC && !S.lite)
     hipExtLaunchKernelGGL((tick_kernel<N, false, SPEC, false, true>), dim3(waves), dim3(64),
                           block_lds_bytes<N, SPEC, true>(), st, ev0, ev1, 0, S, t0, nt);

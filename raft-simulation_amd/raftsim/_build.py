@@ -15,6 +15,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent.parent.parent
 KERNEL_SOURCES = ["raft-simulation_amd/csrc/tick_kernel.hip",
                   "raft-simulation_amd/csrc/steady_kernel.hip",
+                  "raft-simulation_amd/csrc/storm_kernel.hip",
                   "raft-simulation_amd/csrc/tick_wave.hpp", "raft-simulation_amd/csrc/device.hpp",
                   "raft-simulation_amd/csrc/raftsim.hip", "include/raftsim.h"]
 _TAG = re.compile(rb"RAFTSIM_SRC_HASH=([0-9a-f]{16}|unknown)")
