@@ -196,6 +196,27 @@ def test_gpu_storm_window(variant, nodes):
     assert np.array_equal(g2.digest(), r2.digest())
 
 
+@pytest.mark.parametrize("variant,inbox", [(0, 16), (2, 2)])
+def test_gpu_storm_engine(variant, inbox):
+    """The storm kernel (storm_kernel.hip, one lane per cluster; handles of 131,072 clusters or
+    more): storm launches split into chunks (rings carried across launches), with a two-message
+    inbox whose overflowing clusters are rerun by the lane-per-node STORM body; digest- and
+    counter-equal to the oracle through the storm ticks and the elections after them
+    (core.clj:151-160, server.clj:62-63)."""
+    cfg = dict(n_clusters=131072, nodes=5, seed=21 + variant, el_base=3000, el_span=2000,
+               client_ppm=200000, client_period=8192, client_burst=2048, client_redirects=4,
+               inbox_cap=inbox, log_cap=128, variant_flags=variant, drop_ppm=100000, dmin=1,
+               dmax=30, part_ppm=50000)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    for _ in range(4):
+        g.step(1250)
+        r.step(1250)
+        bad = np.nonzero(g.digest() != r.digest())[0]
+        assert not len(bad), f"tick {g.tick}: {len(bad)} clusters differ, first {bad[0]}"
+    assert g.counters() == r.counters()
+
+
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
 def test_gpu_init_election_closed_form(nodes, d):
     """The steady kernel's election from init-node (steady_kernel.hip) for every follower count
@@ -514,6 +535,27 @@ def test_gpu_storm_window(variant, nodes):
     helpers.oracle_threads(r2, helpers.cpu_threads())
     r2.step(4000)
     assert np.array_equal(g2.digest(), r2.digest())
+
+
+@pytest.mark.parametrize("variant,inbox", [(0, 16), (2, 2)])
+def test_gpu_storm_engine(variant, inbox):
+    """The storm kernel (storm_kernel.hip, one lane per cluster; handles of 131,072 clusters or
+    more): storm launches split into chunks (rings carried across launches), with a two-message
+    inbox whose overflowing clusters are rerun by the lane-per-node STORM body; digest- and
+    counter-equal to the oracle through the storm ticks and the elections after them
+    (core.clj:151-160, server.clj:62-63)."""
+    cfg = dict(n_clusters=131072, nodes=5, seed=21 + variant, el_base=3000, el_span=2000,
+               client_ppm=200000, client_period=8192, client_burst=2048, client_redirects=4,
+               inbox_cap=inbox, log_cap=128, variant_flags=variant, drop_ppm=100000, dmin=1,
+               dmax=30, part_ppm=50000)
+    g, r = helpers.gpu(**cfg), helpers.oracle(**cfg)
+    helpers.oracle_threads(r, helpers.cpu_threads())
+    for _ in range(4):
+        g.step(1250)
+        r.step(1250)
+        bad = np.nonzero(g.digest() != r.digest())[0]
+        assert not len(bad), f"tick {g.tick}: {len(bad)} clusters differ, first {bad[0]}"
+    assert g.counters() == r.counters()
 
 
 @pytest.mark.parametrize("nodes,d", [(2, 1), (3, 2), (4, 1), (5, 3), (5, 1)])
