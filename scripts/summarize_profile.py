@@ -36,9 +36,31 @@ def is_steady(name):
     return any(s in name for s in STEADY)
 
 
+# storm launches: the lane-per-cluster storm kernel, then the general STORM body over the clusters
+# it listed (storm_kernel.hip): two dispatches, one launch
+STORM = "storm_lane_kernel"
+
+
+def is_tick(name):
+    return is_steady(name) or KERNEL in name or STORM in name
+
+
 def launch_groups(rows, name_key):
-    """Dispatch-ordered rows as tick launches: one dispatch each (steady or general)."""
-    return [[r] for r in rows if is_steady(r[name_key]) or KERNEL in r[name_key]]
+    """Dispatch-ordered rows as tick launches: one dispatch each (steady or general), or a storm
+    kernel with the tick-kernel dispatch that follows it."""
+    out, rerun = [], False
+    for r in rows:
+        name = r[name_key]
+        if STORM in name:
+            out.append([r])
+            rerun = True
+        elif is_steady(name) or KERNEL in name:
+            if rerun:
+                out[-1].append(r)
+            else:
+                out.append([r])
+            rerun = False
+    return out
 
 
 def counters_by_kernel(path):
@@ -103,7 +125,7 @@ def main():
         # one value per counter per dispatch, then summed over each launch's dispatches
         disp = collections.OrderedDict()
         for r in rows:
-            if KERNEL in r["Kernel_Name"] or is_steady(r["Kernel_Name"]):
+            if is_tick(r["Kernel_Name"]):
                 e = disp.setdefault(r["Dispatch_Id"], {"Kernel_Name": r["Kernel_Name"], "c": {}})
                 e["c"][r["Counter_Name"]] = e["c"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         for g in launch_groups(list(disp.values()), "Kernel_Name"):
@@ -119,7 +141,7 @@ def main():
     groups = launch_groups(trace, "Kernel_Name")
     durs = [int(g[-1]["End_Timestamp"]) - int(g[0]["Start_Timestamp"]) for g in groups]
     stats = [r for r in csv.DictReader(open(src / "kt" / "run_kernel_stats.csv"))
-             if KERNEL in r["Name"] or is_steady(r["Name"])]
+             if is_tick(r["Name"])]
     durs = durs[-max(1, bench["roofline"]["launches"]):]   # the timed launches, not the warm-up
     avg_ns = sum(durs) / max(1, len(durs))
 
