@@ -88,17 +88,21 @@ def C4_CFG(nodes, seed):
 # steps) after a warm-up step for "steady" windows; for "init" windows cluster-steps, i.e. the
 # oracle runs cluster_steps // steps clusters over the GPU's own window from init-node.
 WORKLOADS = {
-    "c2": dict(cfg=dict(nodes=5, seed=42), clusters=65536, scaling="weak", window="steady",
+    "c2": dict(short="C2: 65,536 5-node clusters/GPU, 10k ticks/step, no faults, no client (steady window)",
+               cfg=dict(nodes=5, seed=42), clusters=65536, scaling="weak", window="steady",
                cpu=(65536, 40),
                desc="C2: 65,536 five-node clusters per GPU x 10,000 ticks per step, no faults, "
                     "no client"),
-    "c2_init": dict(cfg=dict(nodes=5, seed=42), clusters=65536, scaling="weak", window="first",
+    "c2_init": dict(short="C2 from init-node: ticks [0,10k), first elections",
+                    cfg=dict(nodes=5, seed=42), clusters=65536, scaling="weak", window="first",
                     cpu=65536, reps=5,
                     desc="C2 as named: 65,536 five-node clusters per GPU, ticks [0, 10,000) from "
                          "init-node (first elections included), no faults, no client"),
-    "c3": dict(cfg=C3_CFG, clusters=1 << 20, scaling="strong", window="init", cpu=1 << 19,
+    "c3": dict(short="C3: 1M 5-node clusters, drop/dup/delay/partitions, bursty redirecting client, [0,10k*K) from init",
+               cfg=C3_CFG, clusters=1 << 20, scaling="strong", window="init", cpu=1 << 19,
                desc="C3: " + C3_DESC),
-    "c3_spec": dict(cfg=dict(C3_CFG, variant_flags=2, log_cap=1024), clusters=1 << 20,
+    "c3_spec": dict(short="C3 under Spec-Raft",
+                    cfg=dict(C3_CFG, variant_flags=2, log_cap=1024), clusters=1 << 20,
                     scaling="strong", window="init", cpu=1 << 19,
                     desc="C3 under the Spec-Raft control (SIM_SPEC §8, 1024-entry logs): "
                          + C3_DESC),
@@ -106,16 +110,20 @@ WORKLOADS = {
     # the 1000+-entry AppendEntries batches (core.clj:56-67 ships the whole suffix, log.clj:61-64)
     # and the OVERFLOW halts at the 4096-entry cap; Spec-Raft is where the commit index comes from
     # the sorting network over match_index
-    "c4_n7": dict(cfg=C4_CFG(7, 3), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
+    "c4_n7": dict(short="C4: 16,384 7-node clusters/GPU, 4096-entry logs, bursty client, from init",
+                  cfg=C4_CFG(7, 3), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
                   desc="C4: 16,384 seven-node clusters per GPU, " + C4_DESC),
-    "c4_n9": dict(cfg=C4_CFG(9, 5), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
+    "c4_n9": dict(short="C4: 16,384 9-node clusters/GPU, 4096-entry logs, bursty client, from init",
+                  cfg=C4_CFG(9, 5), clusters=16384, scaling="weak", window="init", cpu=1 << 15,
                   desc="C4: 16,384 nine-node clusters per GPU, " + C4_DESC),
-    "c4_spec": dict(cfg=dict(C4_CFG(9, 5), variant_flags=2), clusters=16384, scaling="weak",
+    "c4_spec": dict(short="C4-N9 under Spec-Raft (sorting-network commit)",
+                    cfg=dict(C4_CFG(9, 5), variant_flags=2), clusters=16384, scaling="weak",
                     window="init", cpu=1 << 15,
                     desc="C4 under the Spec-Raft control (majority commit index by the sorting "
                          "network over match_index, truncate-on-conflict): 16,384 nine-node "
                          "clusters per GPU, " + C4_DESC),
-    "c5": dict(cfg=dict(C3_CFG, variant_flags=3, log_cap=1024), clusters=131072, scaling="weak",
+    "c5": dict(short="C5: 131,072 clusters/GPU, no-log-check vote variant, to first violation",
+               cfg=dict(C3_CFG, variant_flags=3, log_cap=1024), clusters=131072, scaling="weak",
                window="violation", chunk=1000, max_ticks=200000,
                desc="C5: 131,072 five-node clusters per GPU with C3's faults and client, Spec-Raft "
                     "with the vote granted without the up-to-date check (variant flags 3); "
@@ -123,6 +131,14 @@ WORKLOADS = {
                     "counted anywhere in the job"),
 }
 HALTS = ("halt_ioobe", "halt_npe", "halt_cce", "halt_overflow")
+MODEL = {
+    "steady": "frac: compulsory bytes (hot state in+out, 2(32+8N) B/node) / launch; frac_measured: "
+              "PMC HBM bytes / launch. The 42 MB state stays Infinity-Cache resident between "
+              "launches and the launch is dispatch-bound (~3 us empty dispatch + one wave's chain)",
+    "general": "frac: compulsory bytes (hot state in+out, 2(32+8N) B/node) / launch; frac_measured: "
+               "PMC HBM bytes / launch. Bound by the issue of divergent per-trip instruction "
+               "streams, not HBM bandwidth",
+}
 LIMITER = {
     "steady": "one wave per SIMD running 64 clusters' heartbeat rounds (C2 has exactly 64 clusters "
               "per SIMD): the state load, the chain of dependent multiplies per trip (trace hash; "
@@ -155,6 +171,14 @@ def window_id(spec, args):
 def load_traffic(workload, window):
     """PMC HBM bytes per tick-kernel launch measured on THIS kernel source over this window (else
     None, with the reason)."""
+    rec, why = load_pmc(workload, window)
+    return (rec.get("hbm_bytes_per_launch"), rec.get("source")) if rec else (None, why)
+
+
+def load_pmc(workload, window):
+    """The pmc_traffic.json record of `workload` (HBM bytes, LDS bank conflicts, occupancy per
+    tick-kernel launch) if it was measured on THIS kernel source over this window, else (None, the
+    reason)."""
     f = ROOT / "pmc_traffic.json"     # written by scripts/summarize_profile.py
     try:
         rec = json.loads(f.read_text()).get(workload)
@@ -166,7 +190,7 @@ def load_traffic(workload, window):
         return None, "PMC profile of another kernel build"
     if rec.get("window") != window:
         return None, f"PMC profile window {rec.get('window')} is not this window"
-    return rec.get("hbm_bytes_per_launch"), rec.get("source")
+    return rec, rec.get("source")
 
 
 def host_cpus():
@@ -221,6 +245,7 @@ def cpu_baseline(spec, args):
                       f"with the same idle-tick skipping as the kernel, {threads} threads (the host "
                       f"CPUs this process may use: affinity mask capped by the cgroup quota), "
                       f"{dt:.2f} s",
+            "short_sample": f"{clusters} clusters, {where}, oracle/raftref.c, {threads} threads",
             "host_cpus": hc,
             "every_tick_value": v_every,
             "every_tick_sample": f"{max(1, clusters // 8)} clusters x 1 step visiting every tick, "
@@ -238,14 +263,20 @@ def roofline(name, spec, count, n, launches, avg_launch_ms, delta, window, world
     state_bytes = 2 * s_node * count * n
     event_bytes = state_bytes + 64 * msgs + 16 * entries
     gbs = (lambda b: b / (avg_launch_ms * 1e-3) / 1e9) if avg_launch_ms else (lambda b: 0.0)
-    traffic, traffic_src = load_traffic(name, window)
+    pmc, traffic_src = load_pmc(name, window)
+    pmc = pmc or {}
+    traffic = pmc.get("hbm_bytes_per_launch")
     steady = spec["cfg"]["nodes"] <= 5 and not spec["cfg"].get("client_ppm") and \
         spec["window"] in ("steady",)
     return {"bound": "hbm", "achieved": gbs(state_bytes), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": gbs(state_bytes) / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_source": traffic_src,
-            "model": "compulsory: the hot node state in and out once, 2 * S_node * nodes per "
-                     "launch (S_node = 32 + 8N bytes)",
+            # the PMC-measured bytes over the same launch time: what the memory system moved
+            "frac_measured": gbs(traffic) / HBM_PEAK_GBS if traffic else None,
+            "lds_bank_conflict_per_lds_inst": pmc.get("lds_bank_conflict_per_lds_inst"),
+            "waves_per_simd": pmc.get("waves_per_simd"),
+            "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
+            "model": MODEL["steady" if steady else "general"],
             "bytes_per_launch": state_bytes, "avg_launch_ms": avg_launch_ms,
             "avg_launch_source": launch_src,
             "traffic_over_compulsory": traffic / state_bytes if traffic else None,
@@ -507,6 +538,8 @@ def main():
                     help="headline[+extra...] from " + ", ".join(WORKLOADS))
     ap.add_argument("--clusters", type=int, default=0, help="override the headline's clusters")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-json", default=None,
+                    help="where the full per-workload records go (default gpurun_out/bench_full.json)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -523,33 +556,85 @@ def main():
     names = args.workload.split("+")
     recs = {name: run_workload(name, args, world, rank, local_rank, dist) for name in names}
     if rank == 0:
-        head = recs[names[0]]
-        out = {
-            "metric": "simulated node-ticks/sec (5-node Raft)" if WORKLOADS[names[0]]["cfg"]["nodes"] == 5
-            else "simulated node-ticks/sec",
-            "value": head["value"],
-            "unit": "node-ticks/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": head["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": head["scaling"],
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (seeded Philox clusters from init-node state)",
-            "config": head["config"],
-            "roofline": head["roofline"],
-        }
-        for k in ("wall_ms_per_step", "wall_value", "timing", "window", "timed_launch_ms",
-                  "timed_launches", "events_per_s", "payload_evicted", "counters", "cpu_baseline"):
-            if k in head:
-                out[k] = head[k]
-        if len(names) > 1:
-            out["workloads"] = {name: recs[name] for name in names[1:]}
-        print(json.dumps(out), flush=True)
+        full = args.full_json or str(ROOT / "gpurun_out" / "bench_full.json")
+        try:
+            Path(full).parent.mkdir(parents=True, exist_ok=True)
+            Path(full).write_text(json.dumps({"n_gpus": world, "steps": args.steps,
+                                              "warmup": args.warmup, "workloads": recs},
+                                             indent=1) + "\n")
+        except OSError as e:                      # the full record is a convenience; the line is not
+            print(f"bench: could not write {full}: {e}", file=sys.stderr)
+            full = None
+        print(json.dumps(compact_line(names, recs, world, args, full)), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _r(x, d=4):
+    """Round for the line: floats to d significant digits (the driver keeps ~8 KB of stdout)."""
+    if isinstance(x, float):
+        return float(f"{x:.{d}g}")
+    return x
+
+
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "frac_measured", "traffic",
+             "traffic_over_compulsory", "bytes_per_launch", "avg_launch_ms",
+             "lds_bank_conflict_per_lds_inst", "waves_per_simd")
+WL_KEYS = ("value", "ms_per_step", "live_node_frac_end", "ev_ae", "payload_max",
+           "first_violation_tick", "time_to_first_violation_s")
+
+
+def compact_line(names, recs, world, args, full_path):
+    """The ONE JSON line bench.py prints: the headline workload's keys, its roofline and CPU
+    baseline, and per workload only its rate, step time, roofline fractions and traffic, CPU rate
+    and the fields that say what the window held; the full records go to `full_path`. Kept well
+    under 8,000 characters (tests/test_bench_contract.py)."""
+    head = recs[names[0]]
+    n = WORKLOADS[names[0]]["cfg"]["nodes"]
+    out = {
+        "metric": "simulated node-ticks/sec (5-node Raft)" if n == 5 else "simulated node-ticks/sec",
+        "value": _r(head["value"], 6),
+        "unit": "node-ticks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": _r(head["ms_per_step"], 6),
+        "higher_is_better": True,
+        "scaling": head["scaling"],
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded Philox clusters from init-node state)",
+        "config": {"workload": WORKLOADS[names[0]]["short"],
+                   **{k: head["config"][k] for k in ("clusters", "clusters_per_gpu", "nodes",
+                                                      "parallelism")}},
+        "roofline": {k: _r(head["roofline"].get(k)) for k in ROOF_KEYS},
+        "wall_ms_per_step": _r(head.get("wall_ms_per_step")),
+        "events_per_s": _r(head.get("events_per_s")),
+    }
+    out["roofline"]["model"] = head["roofline"]["model"]
+    if "timed_launch_ms" in head:
+        out["timed_launch_ms"] = _r(head["timed_launch_ms"])
+    cb = head.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {"value": _r(cb["value"]), "unit": cb["unit"], "cores": cb["cores"],
+                               "kind": cb["kind"], "sample": cb.get("short_sample", cb["sample"])}
+    wls = {}
+    for name in names[1:]:
+        r = recs[name]
+        w = {k: _r(r[k]) for k in WL_KEYS if k in r}
+        roof = r["roofline"]
+        for k in ("frac", "frac_measured", "traffic", "lds_bank_conflict_per_lds_inst",
+                  "waves_per_simd"):
+            w[k] = _r(roof.get(k))
+        if "cpu_baseline" in r:
+            w["cpu"] = _r(r["cpu_baseline"]["value"])
+            if "bit_exact" in r["cpu_baseline"]:
+                w["cpu_bit_exact"] = r["cpu_baseline"]["bit_exact"]
+        wls[name] = w
+    if wls:
+        out["workloads"] = wls
+    out["full_record"] = os.path.relpath(full_path, ROOT) if full_path else None
+    return out
 
 
 if __name__ == "__main__":

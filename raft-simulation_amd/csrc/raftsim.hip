@@ -91,6 +91,7 @@ struct Shard {
   // init-node with client traffic, so no timer fires before el_base and the only events are
   // client-sets at followers. Any host write of state or of the clock ends it (0).
   uint32_t storm_until;
+  bool storm_ran = false;              // a storm-kernel launch has run (raftsim_diag_storm_bails)
 };
 constexpr uint32_t STEADY_COOLDOWN = 2;
 // The wave packing is rebuilt every RESORT_EVERY-th tick launch and reused in between: with
@@ -395,6 +396,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
                           (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
 #endif
     s->last_steady = steady;
+    if (storm && !steady && s->d.storm_list && !s->d.TC && !s->d.lite) s->storm_ran = true;
     if (steady) {
       s->d.nbail = s->nbail2 + s->steady_parity;
       s->d.nbail_zero = s->nbail2 + (s->steady_parity ^ 1);
@@ -1095,6 +1097,24 @@ extern "C" int raftsim_diag_last_bails(raft_sim_t* r) {
   return total;
 }
 
+// Diagnostic (not part of include/raftsim.h): clusters the storm kernel listed for the
+// lane-per-node STORM body in the last storm-kernel launch (storm_kernel.hip), summed over shards;
+// -1 if no shard has run one. Tests bound it: a regression that reruns most clusters shows here.
+extern "C" int raftsim_diag_storm_bails(raft_sim_t* r) {
+  if (!r) return fail(-EINVAL, "null sim");
+  int total = 0;
+  bool any = false;
+  for (Shard* s : r->sh) {
+    if (!s->storm_ran) continue;
+    any = true;
+    uint32_t v = 0;
+    HIP_OK(hipSetDevice(s->cfg.device));
+    HIP_OK(hipStreamSynchronize(s->stream));
+    HIP_OK(hipMemcpy(&v, s->d.storm_count, 4, hipMemcpyDeviceToHost));
+    total += (int)v;
+  }
+  return any ? total : -1;
+}
 
 #ifdef RS_WAVELOG
 // Diagnostic builds only (not part of include/raftsim.h): the per-wave timeline of shard 0's last

@@ -28,7 +28,10 @@ def check_build():
     if _checked or "RAFTSIM_LIB" in os.environ:
         return
     want, got = _build.source_hash(), _build.embedded_hash(LIB_PATH)
-    if want is not None and got != want:
+    if want is None:
+        raise RaftSimError("kernel sources missing beside the library: cannot check which sources "
+                           f"{LIB_PATH} was built from")
+    if got != want:
         raise RaftSimError(f"{LIB_PATH} was built from kernel sources {got}, the tree holds "
                            f"{want}: rebuild with __graft_entry__.build()")
     _checked.append(True)
@@ -49,6 +52,17 @@ class Simulator(Backend):
         import ctypes
 
         f = self._lib.raftsim_diag_last_bails
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p]
+        return int(f(self._h))
+
+    def diag_storm_bails(self):
+        """Diagnostic: clusters the storm kernel (storm_kernel.hip) listed for the lane-per-node
+        STORM body in the last storm launch, summed over shards; -1 if no storm-kernel launch ran
+        on this handle."""
+        import ctypes
+
+        f = self._lib.raftsim_diag_storm_bails
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p]
         return int(f(self._h))

@@ -111,8 +111,8 @@ def main():
     dst.mkdir(exist_ok=True)
     shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_{wl}_kernel_stats.csv")
 
-    bench = next(json.loads(l) for l in (src / "kt.log").read_text().splitlines()
-                 if l.startswith('{"metric"'))
+    # the profiled run's full record (bench.py --full-json): the line on stdout is the compact one
+    bench = json.loads((src / "kt_full.json").read_text())["workloads"][wl]
     pmc = collections.defaultdict(list)
     for i in range(1, 20):
         d = src / f"pmc{i}"
@@ -197,7 +197,16 @@ def main():
             "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / waves_ran
             if "SQ_INSTS_VALU" in avg else None,
             "salu_insts_per_wave": avg["SQ_INSTS_SALU"] / waves_ran
-            if "SQ_INSTS_SALU" in avg else None},
+            if "SQ_INSTS_SALU" in avg else None,
+            # SQ_LDS_BANK_CONFLICT: extra LDS cycles from conflicts (MI355X_MICROARCH.md §LDS)
+            "lds_bank_conflict_per_lds_inst": avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_INSTS_LDS"]
+            if avg.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in avg else None,
+            # mean resident waves per SIMD over the launch: SQ_WAVE_CYCLES (quad-cycles summed
+            # over waves) x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)
+            "waves_per_simd": 4 * avg["SQ_WAVE_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            if avg.get("GRBM_GUI_ACTIVE") and "SQ_WAVE_CYCLES" in avg else None,
+            "wait_any_frac": avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
+            if avg.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in avg else None},
         "calibration": {"k_read": k_rd, "k_write": k_wr, "state_read_weight": w_state,
                         "source": f"profiles/{tag}_fetch_calibration.json"},
         "hbm_fetch_bytes_raw": fetch_raw, "hbm_write_bytes_raw": write_raw,
@@ -229,6 +238,10 @@ def main():
                    "compulsory_bytes_per_launch": state_bytes,
                    "traffic_over_compulsory": hbm / state_bytes if state_bytes else None,
                    "traffic_over_event_bytes": hbm / event_bytes if event_bytes else None,
+                   "lds_bank_conflict_per_lds_inst":
+                       out["derived"]["lds_bank_conflict_per_lds_inst"],
+                   "waves_per_simd": out["derived"]["waves_per_simd"],
+                   "valu_insts_per_wave": out["derived"]["valu_insts_per_wave"],
                    "source": f"profiles/{tag}_{wl}_pmc.json"}
     tf.write_text(json.dumps(traffic, indent=1, sort_keys=True) + "\n")
     print(json.dumps({k: out[k] for k in ("workload", "avg_duration_ns_trace",

@@ -100,3 +100,86 @@ def test_traffic_only_from_the_same_sources_and_window(bench, tmp_path, monkeypa
     (tmp_path / bench.KERNEL_SOURCES[0]).write_text("edited")              # another build
     assert bench.load_traffic("c2", win) == (None, "PMC profile of another kernel build")
 
+
+
+def _worst_case_record(bench, name, world):
+    """A record shaped like run_workload's, every field present and every float at full
+    precision, with long prose and a full counter dict (the round-5 line was 24 KB of these)."""
+    spec = bench.WORKLOADS[name]
+    long = "x" * 400
+    counters = {f"counter_{i}": 123456789012345 + i for i in range(40)}
+    roof = {k: 0.123456789012345 for k in ("achieved", "frac", "frac_measured", "traffic",
+                                           "traffic_over_compulsory", "avg_launch_ms",
+                                           "lds_bank_conflict_per_lds_inst", "waves_per_simd",
+                                           "frac_event_model", "event_bytes_per_launch")}
+    roof.update(bound="hbm", peak=8000.0, unit="GB/s", bytes_per_launch=755000000,
+                model=bench.MODEL["general"], traffic_source=long, avg_launch_source=long,
+                limiter=long, kernel_src_sha="0" * 16, launches=20,
+                survey_8d={"value": 1.0, "note": long})
+    rec = {"value": 3.901234567890123e14, "unit": "node-ticks/s", "ms_per_step": 0.00841234567,
+           "wall_ms_per_step": 0.123456789, "wall_value": 1.23456789e13, "timing": long,
+           "scaling": spec["scaling"], "window": {"kind": "init", "steps": 20},
+           "config": {"workload": spec["desc"], "clusters": spec["clusters"] * world,
+                      "clusters_per_gpu": spec["clusters"], "nodes": spec["cfg"]["nodes"],
+                      "ticks_per_step": 10000, "parallelism": f"cluster-sharded x{world}"},
+           "roofline": roof, "events_per_s": 2.4123456789e11, "live_node_frac_end": 0.15812345,
+           "live_node_ticks_per_s": 6.9812345e10, "payload_evicted": 0, "ev_ae": 655360,
+           "payload_max": 2156, "counters": counters, "timed_launch_ms": 0.008123456,
+           "timed_launches": 1, "first_violation_tick": 16572, "time_to_first_violation_s": 0.015,
+           "cpu_baseline": {"value": 1.8912345e11, "unit": "node-ticks/s", "cores": 16,
+                            "kind": "port", "sample": long, "short_sample": "y" * 90,
+                            "host_cpus": {"affinity": 16}, "every_tick_value": 1.5e9,
+                            "every_tick_sample": long, "bit_exact": True}}
+    return rec
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_bench_line_fits_the_drivers_tail(bench, world):
+    """the driver keeps ~8,000 characters of stdout and parses the last line,
+    so the one JSON line must stay well under that with every workload on it; the headline keys,
+    roofline and cpu_baseline are on it and n_gpus / parallelism follow the world size."""
+    src = (ROOT / "bench.py").read_text()
+    default = next(l.split('default="', 1)[1].split('"', 1)[0] for l in src.splitlines()
+                   if '"--workload"' in l)
+    names = default.split("+")
+    recs = {n: _worst_case_record(bench, n, world) for n in names}
+    args = SimpleNamespace(steps=20, warmup=5)
+    out = bench.compact_line(names, recs, world, args, str(ROOT / "gpurun_out" / "bench_full.json"))
+    line = json.dumps(out)
+    assert len(line) < 6000, len(line)
+    assert "\n" not in line
+    back = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
+              "cpu_baseline", "workloads"):
+        assert k in back, k
+    assert back["n_gpus"] == world
+    assert back["config"]["parallelism"] == f"cluster-sharded x{world}"
+    for k in ("frac", "achieved", "peak", "traffic", "frac_measured",
+              "lds_bank_conflict_per_lds_inst", "waves_per_simd", "model"):
+        assert k in back["roofline"], k
+    assert {"value", "cores", "kind"} <= set(back["cpu_baseline"])
+    assert set(back["workloads"]) == set(names[1:])
+    for w in back["workloads"].values():
+        assert {"value", "ms_per_step", "frac", "traffic", "cpu"} <= set(w)
+    assert back["full_record"] == "gpurun_out/bench_full.json"
+
+
+def test_pmc_record_feeds_occupancy_and_conflicts(bench, tmp_path, monkeypatch):
+    """roofline carries the same-sha profile's LDS bank conflicts and waves per SIMD, and
+    frac_measured = PMC bytes / launch time / peak beside the compulsory frac."""
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    for f in bench.KERNEL_SOURCES:
+        p = tmp_path / f
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text("kernel source " + f)
+    win = {"kind": "steady", "steps": 20, "warmup": 5}
+    rec = {"c2": {"kernel_src_sha": bench.kernel_build_hash(), "window": win,
+                  "hbm_bytes_per_launch": 25.6e6, "source": "profiles/x.json",
+                  "lds_bank_conflict_per_lds_inst": 0.01, "waves_per_simd": 0.9}}
+    (tmp_path / "pmc_traffic.json").write_text(json.dumps(rec))
+    r = bench.roofline("c2", bench.WORKLOADS["c2"], 65536, 5, 20, 0.008, {"delivered": 0,
+                       "entries_appended": 0}, win, 1)
+    assert r["frac_measured"] == pytest.approx(25.6e6 / 8e-6 / 1e9 / 8000)
+    assert r["lds_bank_conflict_per_lds_inst"] == 0.01 and r["waves_per_simd"] == 0.9
+    assert "Infinity-Cache" in r["model"]
