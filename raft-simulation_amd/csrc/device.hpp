@@ -392,8 +392,11 @@ __device__ __forceinline__ uint2* arena_of(const DevSim& S, uint32_t gi) {
   return reinterpret_cast<uint2*>(S.arena) + (size_t)gi * S.A;
 }
 
+#ifndef RS_KO_CTR
+#define RS_KO_CTR 0     // knock-out switch of timing-only diagnostic builds: never set in the product
+#endif
 __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
-  if (v) atomicAdd(&lctr[i], v);
+  if (!RS_KO_CTR && v) atomicAdd(&lctr[i], v);
 }
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own

@@ -12,6 +12,18 @@
 
 namespace rs {
 
+#ifndef RS_PROV
+#define RS_PROV 1
+#endif
+
+// knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
+#ifndef RS_KO_P4
+#define RS_KO_P4 0
+#endif
+#ifndef RS_KO_LOGM
+#define RS_KO_LOGM 0
+#endif
+
 __device__ __forceinline__ void violation(uint32_t* lctr, int kind, uint32_t t) {
   atomicAdd(&lctr[kind], 1u);
   atomicMin(&lctr[LCTR_FIRSTVIOL], t);
@@ -460,6 +472,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr int CPW = 64 / N;
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
+  // payload provenance for the checker (below): the kernels with long replicated runs
+  constexpr bool PROV = RS_PROV && !LITE && !STORM && (SPEC || N >= 6);
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -501,6 +515,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
 
     NodeR n = {};
     uint32_t hidx = 0, hterm = 0, hval = 0;   // checker high-water mark (cluster-replicated)
+    // Payload provenance (PROV; launch-local, not state). Arena slots are written only at a
+    // node's frontier, so an entry copied from sender S's arena at absolute position key + p
+    // (key = source offset - appended_at) without eviction equals every other unevicted copy of
+    // that slot. pk = key and pm = S | from << 4 | to << 18 of the lane's last payload append
+    // (pm = 0: none, or an eviction): its log positions [from, to) hold S's slots key + p. Later
+    // entry appends land at to or past it, remove-from! clamps to, a payload append replaces both.
+    // The checker then skips a pair whose positions are such copies on both sides (P4).
+    uint32_t pk = 0, pm = 0;
     uint32_t cnext = INF, ccount = 0;         // client-set injection cursor (cluster-replicated)
     if (active) {
       const uint32_t fl = hp[HF_FLAGS * N], mk = hp[HF_MASKS * N], qm = hp[HF_QMETA * N];
@@ -946,6 +968,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
               } else if (!consistent) {
                 ra = make_uint4(RAFT_MSG_APPEND_RESPONSE | id << 3, n.term, 0, 0);
                 n.len = n.len > mb ? n.len - mb : 0;          // remove-from! 78-81
+                if constexpr (PROV) {
+                  if ((pm >> 18) > n.len) pm = (pm & 0x3FFFFu) | n.len << 18;
+                }
                 n.seq = 1;
               } else {
                 if (n.len + pcnt > kargs()->L) {
@@ -1294,6 +1319,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             }
             arena_copy<LITE ? 1 : 8>(sar, di, sa, si, m - evicted, A);
             lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, evicted);
+            if constexpr (PROV) {
+              pk = ppoff - pold_len;
+              pm = evicted == 0 && n.len < (1u << 14) ? psrc | pold_len << 4 | n.len << 18 : 0u;
+            }
           }
         }
         if (papplied) {          // apply-entries! writes the last `applied` :val's (log.clj:69-76)
@@ -1330,7 +1359,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // ---------------------------------------------------------------- P4 invariant checker
       // the majority-match scan can raise hwm only when the leader's log reaches past it
       const bool mcheck = (elected || mchg) && n.len > hidx;
-      if (!STORM && __ballot(elected || appended_at >= 0 || mcheck)) {
+      if (!RS_KO_P4 && !STORM && __ballot(elected || appended_at >= 0 || mcheck)) {
         if (__ballot(elected)) {                       // election safety
           bool bad = false;
   #pragma unroll
@@ -1340,7 +1369,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           }
           if (bad) violation(lctr, RAFT_CTR_VIOL_ELECTION, t);
         }
-        if (__ballot(appended_at >= 0)) {              // log matching
+        if (!RS_KO_LOGM && __ballot(appended_at >= 0)) {              // log matching
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // peers' P3 arena writes
           // Each lane b compares its own log with the new entries of every other node a of its
           // cluster that appended this tick, pair after pair, W positions per trip of one
@@ -1364,6 +1393,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           apw[lane] = (uint32_t)appended_at;
           apw[64 + lane] = n.base;
           apw[128 + lane] = n.len;
+          if constexpr (PROV) {   // this tick's payload append and its provenance (0: none)
+            apw[320 + lane] = appended_at >= 0 && pkind == PLAN_PAYLOAD ? pm : 0u;
+            apw[384 + lane] = pk;
+          }
           const uint32_t apc = (uint32_t)(__ballot(active && appended_at >= 0) >> bl) & cmask;
           constexpr int W = LITE ? 1 : 8;
           uint32_t found = 0;
@@ -1395,6 +1428,19 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                   }
                   if (asrc && pay && psrc == asrc && ppoff - (uint32_t)appended_at == akey)
                     hi = min(hi, (uint32_t)appended_at);     // where this lane holds the same copy
+                }
+                if constexpr (PROV) {
+                  // a's new entries are copies of S's slots akey + p: equal to this lane's
+                  // entries when this lane is S at base akey (its log position p is slot
+                  // base + p), or when its positions [aat, hi) are copies of the same slots
+                  const uint32_t am = apw[320 + bl + a];
+                  if (am) {
+                    const uint32_t akey = apw[384 + bl + a];
+                    const bool same = ((am & 15) == id && akey == n.base) ||
+                                      ((pm & 15) == (am & 15) && pk == akey &&
+                                       ((pm >> 4) & 0x3FFFu) <= aat && hi <= (pm >> 18));
+                    if (same) hi = aat;
+                  }
                 }
                 todo &= ~grp;
                 rem = hi > aat ? hi - aat : 0u;

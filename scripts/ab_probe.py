@@ -18,6 +18,12 @@ WORK = {
                **FAULTS),
     "c4_n9": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=500000, log_cap=4096,
                   client_period=8192, client_burst=2048, client_redirects=4),
+    "c4_n7": dict(n_clusters=16384, nodes=7, seed=3, client_ppm=500000, log_cap=4096,
+                  client_period=8192, client_burst=2048, client_redirects=4),
+    "c4_spec": dict(n_clusters=16384, nodes=9, seed=5, client_ppm=500000, log_cap=4096,
+                    client_period=8192, client_burst=2048, client_redirects=4, variant_flags=2),
+    "c3_spec": dict(n_clusters=131072, nodes=5, seed=1, client_ppm=80000, log_cap=1024, **BURSTS,
+                    **FAULTS, variant_flags=2),
 }
 
 
