@@ -237,7 +237,7 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   d.client_pw = s->client_pw;
   d.wavelog = nullptr;
 #ifdef RS_WAVELOG
-  if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 8))) {
+  if ((rc = dalloc(s, &d.wavelog, (size_t)rs::sched_slots_bound(s->C, s->N) * 12))) {
     sh_destroy(s);
     return rc;
   }
@@ -393,7 +393,7 @@ static int sh_step_async(Shard* s, uint32_t n_ticks) {
     }
 #ifdef RS_WAVELOG
     HIP_OK(hipMemsetAsync(s->d.wavelog, 0,
-                          (size_t)rs::sched_slots_bound(s->C, s->N) * 128 / (64 / s->N), s->stream));
+                          (size_t)rs::sched_slots_bound(s->C, s->N) * 192 / (64 / s->N), s->stream));
 #endif
     s->last_steady = steady;
     if (storm && !steady && s->d.storm_list && !s->d.TC && !s->d.lite) s->storm_ran = true;
@@ -1125,7 +1125,7 @@ extern "C" int raftsim_diag_wavelog(raft_sim_t* r, uint32_t* out, uint32_t cap_w
   const uint32_t waves = rs::sched_slots_bound(s->C, s->N) / (64 / s->N);
   const uint32_t n = std::min(waves, cap_waves);
   HIP_OK(hipSetDevice(s->cfg.device));
-  HIP_OK(hipMemcpy(out, s->d.wavelog, (size_t)n * 128, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(out, s->d.wavelog, (size_t)n * 192, hipMemcpyDeviceToHost));
   return (int)n;
 }
 #endif

@@ -637,7 +637,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // P1's queue pop, 2 the handler, 10 timer/hash/counters, 3 redirects, emission and fault
     // draws, 4 P2, 5 P3, 6 P4, 7 the append-response drain, 8 the trip's loop head (next event,
     // exit ballot); 9 the launch-start state load
-    uint32_t wl_ph[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t wl_ph[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     // wave-level passes of each Philox call site (the first active lane counts the pass; summed
     // over the lanes at the end): 0 client, 1 deferred timer, 2 alts!!, 3 Spec re-arm, 4 redirect, 5 partition,
     // 6 fault draws of replies, 7 fault draws of broadcasts (per peer)
@@ -1158,6 +1158,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // The message words go to the pair cells, then each message's fault draws (its delivery
           // pack, in the cell's last word) and the receiver's bit into sentmask.
           if (!STORM && emit) {
+            RS_PHASE(13);
             // the cluster's partition draw for this tick's epoch, made once per epoch (SIM_SPEC P2)
             uint32_t pstate = 0;
             if (!LITE && kargs()->part_ppm) {
@@ -1174,6 +1175,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 pcache[CPW + cw] = pstate;
               }
             }
+            RS_PHASE(14);
             *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
                 emit == 2 ? make_uint2(n.term, n.commit) : make_uint2(ra.y, ra.z);
             if (emit == 3) {
@@ -1239,6 +1241,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   #pragma unroll
                 for (int j = 0; j < N - 1; ++j) cell_put(mycells + (k * (N - 1) + j) * CELLW, ra, rb);
               }
+              RS_PHASE(15);
               if (pmax) atomicMax(&lctr[LCTR_PAYLOADMAX], pmax);
               lctr_add(lctr, RAFT_CTR_SENT, N - 1);
   #pragma unroll 1
@@ -1250,6 +1253,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 if (pack >> 16) sentmask |= 1u << p;
               }
             }
+            RS_PHASE(16);
           }
         }
       }
@@ -1676,7 +1680,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       uint32_t hw, xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 32);
+      uint4* rec = reinterpret_cast<uint4*>(S.wavelog + (size_t)wave * 48);
       rec[0] = make_uint4((uint32_t)wl_start, (uint32_t)(wl_start >> 32), (uint32_t)wl_end,
                           (uint32_t)(wl_end >> 32));
       rec[1] = make_uint4(wl_active, hw, xcc, (wl_kmax - wl_kmin) << 16 | (wl_first & 0xFFFF));
@@ -1686,6 +1690,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       rec[5] = make_uint4(wl_drain, wl_inj, wl_dead, wl_ph[12]);
       rec[6] = make_uint4(wl_px[0], wl_px[1], wl_px[2], wl_px[3]);
       rec[7] = make_uint4(wl_px[4], wl_px[5], wl_px[6], wl_px[7]);
+      rec[8] = make_uint4(wl_ph[13], wl_ph[14], wl_ph[15], wl_ph[16]);
     }
   #endif
 

@@ -25,9 +25,9 @@ sim = Backend(lib, "raft_sim_", n_clusters=C, **CFG)
 for _ in range(LAUNCHES):                       # from init-node, as the bench's C3 window
     sim.step(10000)
 waves = 2 * C // (64 // CFG["nodes"]) + 1000    # >= the padded packing's grid
-buf = (ctypes.c_uint32 * (waves * 32))()
+buf = (ctypes.c_uint32 * (waves * 48))()
 n = sim._lib.raftsim_diag_wavelog(sim._h, buf, waves)
-a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 32)[:n].astype(np.int64)
+a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 48)[:n].astype(np.int64)
 a = a[(a[:, 0] | a[:, 1]) != 0]                 # waves that ran (padding waves exit first)
 n = len(a)
 start = (a[:, 0] | (a[:, 1] << 32)); end = (a[:, 2] | (a[:, 3] << 32))
@@ -89,4 +89,6 @@ print("Philox passes per wave (mean): " + "  ".join(
 print("drained ticks per wave p0/10/50/90/99/100:", q(a[:, 20]))
 print("client-injection ticks per wave p0/10/50/90/99/100:", q(a[:, 21]))
 print("dead clusters per wave at launch start p0/10/50/90/99/100:", q(a[:, 22]))
+print("emission sub-phases per trip (partition, reply, bcast words, deliver): " + "  ".join(
+    f"{v:7.0f}" for v in (a[:, 32:36].astype(np.float64) / np.maximum(act, 1)[:, None]).mean(axis=0)))
 print(f"stamped cycles / lifetime cycles (2.4 GHz nominal): {np.median(tot / (life * 2400)):.2f}")
