@@ -260,7 +260,9 @@ static int sh_create(const raft_sim_config_t* cfg, Shard** out) {
   // C4's 16,384 clusters its 256 waves ran 36 ms against the lane-per-node body's 14): below that
   // the storm ticks run the general STORM body.
   // (Its registers hold arrivals below 2^28 and hop counts below 16.)
-  if (s->storm_until && s->C >= 131072 && cfg->el_base < (1u << 28) && cfg->client_redirects < 16 &&
+  uint32_t storm_min = 131072;
+  if (const char* sm = getenv("RAFTSIM_STORM_MIN_CLUSTERS")) storm_min = (uint32_t)strtoul(sm, nullptr, 10);
+  if (s->storm_until && s->C >= storm_min && cfg->el_base < (1u << 28) && cfg->client_redirects < 16 &&
       ((rc = dalloc(s, &s->d.storm_list, s->C)) ||
                          (rc = dalloc(s, &s->d.storm_count, 1)))) {
     sh_destroy(s);
