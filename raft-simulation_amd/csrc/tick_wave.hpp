@@ -15,6 +15,12 @@ namespace rs {
 #ifndef RS_PROV
 #define RS_PROV 1
 #endif
+#ifndef RS_PROV_SEARCH
+#define RS_PROV_SEARCH 1
+#endif
+#ifndef RS_PROV_MIN_N
+#define RS_PROV_MIN_N 6
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -191,7 +197,7 @@ __device__ __forceinline__ void spec_handle(
     uint32_t& fault, uint32_t& ev, int& emit, int& nm, uint4& ra, uint4& rb, uint32_t& appended,
     uint32_t& applied, uint32_t& pkind, uint32_t& psrc, uint32_t& ppoff, uint32_t& ppcnt,
     uint32_t& pold_base, uint32_t& preloc, uint32_t& papplied, bool& elected, bool& mchg,
-    bool& rearm) {
+    bool& rearm, uint32_t pk, uint32_t pm) {
   const uint32_t A = S.A;
   if (which < 0) {
     if (n.role == RAFT_LEADER) {                                  // heartbeat
@@ -262,6 +268,12 @@ __device__ __forceinline__ void spec_handle(
       const int64_t ev64 = (int64_t)sf0 - (int64_t)mpoff - (int64_t)A;
       const uint32_t E = ev64 <= 0 ? 0u : (ev64 >= (int64_t)pcnt ? pcnt : (uint32_t)ev64);
       uint32_t kk = mb;
+      // Payload provenance (tick_wave's PROV): when this node's positions [mb, hi) are unevicted
+      // copies of the same sender slots this payload names (key mpoff - mb) and none of the
+      // payload is evicted, every term agrees and the search ends at hi.
+      if (RS_PROV_SEARCH && E == 0 && pm && (pm & 15) == src && pk == mpoff - mb && ((pm >> 4) & 0x3FFFu) <= mb &&
+          hi <= (pm >> 18))
+        kk = hi > mb ? hi : mb;
       if (kk < hi) {
         uint32_t yi = (n.base + kk) % A, xi = mpoff % A, rem = hi - kk;
         constexpr int W = 8;
@@ -473,7 +485,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr uint32_t ALL = ((1u << (N + 1)) - 1) & ~1u;
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
   // payload provenance for the checker (below): the kernels with long replicated runs
-  constexpr bool PROV = RS_PROV && !LITE && !STORM && (SPEC || N >= 6);
+  constexpr bool PROV = RS_PROV && !LITE && !STORM && (SPEC || N >= RS_PROV_MIN_N);
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -906,7 +918,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         } else if constexpr (SPEC) {
           spec_handle<N, MAJ>(S, n, lsw, sar, fr, lctr, which, id, k, bl, sgi, peers, m0, m1, fault, ev,
                               emit, nm, ra, rb, appended, applied, pkind, psrc, ppoff, ppcnt,
-                              pold_base, preloc, papplied, elected, mchg, rearm);
+                              pold_base, preloc, papplied, elected, mchg, rearm, pk, pm);
         } else if (which < 0) {
           if (n.role == RAFT_LEADER) {                        // heartbeat-handler 162-164
             ev = 7;
