@@ -1507,14 +1507,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         int32_t cm = -1;
         uint32_t ct = 0, cv = 0;
         if (on && n.role == RAFT_LEADER && mcheck) {
+          // {log_len} ∪ match_index of the peers, the own slot holding log_len: the network
+          // sorts the multiset, so the slot order does not matter, and a fixed slot per peer keeps
+          // the array in registers (a running index over the peers put it on the stack)
           int32_t vals[N];
-          vals[0] = (int32_t)n.len;
-          int j = 1;
   #pragma unroll
-          for (int p = 1; p <= N; ++p) {
-            if (p == (int)id) continue;
-            vals[j++] = ((n.keys >> p) & 1) ? lsw.match(p - 1) : 0;
-          }
+          for (int p = 1; p <= N; ++p)
+            vals[p - 1] = p == (int)id ? (int32_t)n.len
+                                       : (((n.keys >> p) & 1) ? lsw.match(p - 1) : 0);
   #pragma unroll
           for (int i = 1; i < N; ++i)
   #pragma unroll

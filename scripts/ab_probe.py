@@ -53,8 +53,8 @@ def main():
         digests = {bytes(s.digest(0, 256)) for s in sims}
         for lib, ts, ws in zip(libs, times, walls):
             print(f"{wname:6s} {Path(lib).name:28s} median {statistics.median(ts):8.3f} ms  "
-                  f"min {min(ts):8.3f} ms  step wall median {statistics.median(ws):8.3f} ms",
-                  flush=True)
+                  f"min {min(ts):8.3f} ms  sum {sum(ts):9.3f} ms  step wall median "
+                  f"{statistics.median(ws):8.3f} ms", flush=True)
         print(f"{wname:6s} builds agree on state: {len(digests) == 1}", flush=True)
         for s in sims:
             s.close()
