@@ -401,10 +401,14 @@ __device__ __forceinline__ void lctr_add(uint32_t* lctr, int i, uint32_t v) {
 
 // Stable insert of message (m0 = arrival,hdr,term,a ; m1 = b,eterm,eval,poff) into the node's own
 // queue `which` (SIM_SPEC §4 P2: after every queued message whose arrival <= the new one).
+// (rdel / rhalt: the caller's register counts of delivered messages and of messages reaching a
+// halted node, or null for the LDS counters)
 __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t fault, int which,
-                                        QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr) {
+                                        QueueR& q, uint4 m0, uint4 m1, uint32_t* lctr,
+                                        uint32_t* rdel = nullptr, uint32_t* rhalt = nullptr) {
   if (fault) {
-    lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
+    if (rhalt) *rhalt += 1;
+    else lctr_add(lctr, RAFT_CTR_TO_HALTED, 1);
     return;
   }
   const uint32_t Q = S.Q;
@@ -435,7 +439,8 @@ __device__ __forceinline__ void qinsert(const DevSim& S, uint32_t gi, uint32_t f
   dp[1] = m1;
   q.c += 1;
   if (pos == 0) q.arr = arr;
-  lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+  if (rdel) *rdel += 1;
+  else lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
 }
 
 }  // namespace rs

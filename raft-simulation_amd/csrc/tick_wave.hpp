@@ -21,6 +21,9 @@ namespace rs {
 #ifndef RS_PROV_MIN_N
 #define RS_PROV_MIN_N 6
 #endif
+#ifndef RS_RC_MIN_N
+#define RS_RC_MIN_N 6
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -486,6 +489,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr uint32_t MAJ = SPEC ? N / 2 + 1 : (N + 1) / 2;   // majority? (core.clj:19-21) / strict
   // payload provenance for the checker (below): the kernels with long replicated runs
   constexpr bool PROV = RS_PROV && !LITE && !STORM && (SPEC || N >= RS_PROV_MIN_N);
+  // RC: the counters a client burst bumps on every trip (client-set events, redirects, deliveries,
+  // appended entries, injections, messages to halted nodes) are kept per lane in registers and
+  // added to the wave's LDS counters once at the end: N >= 6 (three waves per SIMD anyway; C4
+  // -5 %) and Spec-Raft (C3-spec -3 %); the faithful N <= 5 kernel measured the same either way
+  constexpr bool RC = !LITE && !STORM && (SPEC || N >= RS_RC_MIN_N);
+  uint32_t rc_cs = 0, rc_red = 0, rc_del = 0, rc_app = 0, rc_inj = 0, rc_halt = 0;
+  uint32_t* const rdel = RC ? &rc_del : nullptr;
+  uint32_t* const rhalt = RC ? &rc_halt : nullptr;
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -774,7 +785,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           refill_batch(t);
           const uint32_t cw = (uint32_t)bl / N;          // the cluster's wave slot
           const uint64_t heads = __ballot(cinj && k == 0);
-          if (lane == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, (uint32_t)__popcll(heads));
+          if constexpr (RC) rc_inj += (uint32_t)__popcll(heads);        // (wave-uniform)
+          else if (lane == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, (uint32_t)__popcll(heads));
           if (cinj) {
             const uint32_t s = (uint32_t)bl + (ccount - cq_base[cw]);
             if (cq_tgt[s] == id) {
@@ -796,7 +808,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         if (inj) {
           if (live && n.rq.c == 0) dcs = true;
           else qinsert(S, sgi, n.fault, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                       make_uint4(0, 0, 0, 0), lctr);
+                       make_uint4(0, 0, 0, 0), lctr, rdel, rhalt);
         }
       }
 
@@ -849,10 +861,11 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
         if (dcs) {
           if (which == 0) {
             m0 = make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv);
-            lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
+            if constexpr (RC) ++rc_del;
+            else lctr_add(lctr, RAFT_CTR_DELIVERED, 1);
           } else {
             qinsert(S, sgi, 0, 0, n.rq, make_uint4(t, RAFT_MSG_CLIENT_SET, 0, injv),
-                    make_uint4(0, 0, 0, 0), lctr);
+                    make_uint4(0, 0, 0, 0), lctr, rdel, rhalt);
           }
         }
         if (which >= 0 && !(dcs && which == 0)) {
@@ -1129,8 +1142,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             lsw.next(src - 1) = (int32_t)(SPEC ? mb + 1 : mb);
             lsw.match(src - 1) = (int32_t)(SPEC ? mb : ma);
           }
-          lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
-          lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
+          if (RC && ev == RAFT_MSG_CLIENT_SET) ++rc_cs;
+          else lctr_add(lctr, RAFT_CTR_EV_RV + ev - 1, 1);
+          if constexpr (RC) rc_app += appended;
+          else lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, appended);
           lctr_add(lctr, RAFT_CTR_ENTRIES_APPLIED, applied);
           if (elected) {
             lctr_add(lctr, RAFT_CTR_LEADERS, 1);
@@ -1153,7 +1168,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 const uint32_t i = __umulhi(w.z, N - 1);
                 dst = i + 1 < id ? i + 1 : i + 2;
               }
-              lctr_add(lctr, RAFT_CTR_REDIRECTS, 1);
+              if constexpr (RC) ++rc_red;
+              else lctr_add(lctr, RAFT_CTR_REDIRECTS, 1);
               *reinterpret_cast<uint2*>(mysrec + k * SRECW) =
                   make_uint2(dst == id ? mb + 1 : 0u, ma);
               if (dst != id) {
@@ -1298,7 +1314,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           QueueR q = which ? n.rs : n.rq;
           const uint4 q0 = make_uint4(t + d, c0.x, s != k ? sr.x : 0u, sr.y),
                       q1 = make_uint4(c0.y, c1.x, c1.y, c2.x);
-          qinsert(S, sgi, n.fault, which, q, q0, q1, lctr);
+          qinsert(S, sgi, n.fault, which, q, q0, q1, lctr, rdel, rhalt);
           if (which) n.rs = q;
           else n.rq = q;
           if (LITE || ++copy >= (c2.y >> 16)) {   // LITE: one copy per message
@@ -1770,6 +1786,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       }
     }
   } while (CATCH && (wave += wstride) * CPW < nslots);   // the general grid covers every slot
+  if constexpr (RC) {
+    lctr_add(lctr, RAFT_CTR_EV_CS, rc_cs);
+    lctr_add(lctr, RAFT_CTR_REDIRECTS, rc_red);
+    lctr_add(lctr, RAFT_CTR_DELIVERED, rc_del);
+    lctr_add(lctr, RAFT_CTR_ENTRIES_APPENDED, rc_app);
+    lctr_add(lctr, RAFT_CTR_TO_HALTED, rc_halt);
+    if (lane == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, rc_inj);
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   unsigned long long* const ctr = kargs()->ctr + (size_t)(ctr_copy % CTR_COPIES) * CTR_STRIDE;
   if (lane < RAFT_CTR_COUNT) {

@@ -132,3 +132,27 @@ def test_gpu_c5_time_to_violation_bit_exact():
     assert (cfv, cticks) == (fv, ticks)
     assert np.array_equal(g.digest(), r.digest())
     assert g.counters() == r.counters()
+
+
+def test_gpu_bench_line_is_one_parseable_line(tmp_path):
+    """bench.py run as the driver runs it (a child process, C2 headline plus one more workload):
+    stdout ends with ONE JSON line well under the ~8,000 characters the driver keeps, carrying the
+    headline keys, roofline and cpu_baseline; the full records land in --full-json."""
+    import json
+    import subprocess
+    import sys
+
+    full = tmp_path / "full.json"
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--workload", "c2+c4_n9", "--clusters", "4096", "--full-json", str(full)],
+                         capture_output=True, text=True, timeout=600, cwd=str(ROOT))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert lines and len(lines[-1]) < 6000, len(lines[-1]) if lines else None
+    rec = json.loads(lines[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline",
+              "cpu_baseline", "config", "workloads"):
+        assert k in rec, k
+    assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["value"] > 0
+    assert rec["roofline"]["avg_launch_ms"] > 0 and rec["cpu_baseline"]["value"] > 0
+    assert set(json.loads(full.read_text())["workloads"]) == {"c2", "c4_n9"}
