@@ -24,6 +24,9 @@ namespace rs {
 #ifndef RS_RC_MIN_N
 #define RS_RC_MIN_N 6
 #endif
+#ifndef RS_REGS_MIN_N
+#define RS_REGS_MIN_N 6
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -491,12 +494,18 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   constexpr bool PROV = RS_PROV && !LITE && !STORM && (SPEC || N >= RS_PROV_MIN_N);
   // RC: the counters a client burst bumps on every trip (client-set events, redirects, deliveries,
   // appended entries, injections, messages to halted nodes) are kept per lane in registers and
-  // added to the wave's LDS counters once at the end: N >= 6 (three waves per SIMD anyway; C4
-  // -5 %) and Spec-Raft (C3-spec -3 %); the faithful N <= 5 kernel measured the same either way
-  constexpr bool RC = !LITE && !STORM && (SPEC || N >= RS_RC_MIN_N);
+  // added to the wave's LDS counters once at the end: N >= 7 (three waves per SIMD anyway; C4
+  // -5 %) and Spec-Raft (C3-spec -3 %); the faithful N <= 5 kernel measured the same either way,
+  // and the faithful N = 6 kernel keeps its four waves per SIMD without them
+  constexpr bool RC = !LITE && !STORM && (SPEC || (N >= RS_RC_MIN_N && N >= 7));
   uint32_t rc_cs = 0, rc_red = 0, rc_del = 0, rc_app = 0, rc_inj = 0, rc_halt = 0;
   uint32_t* const rdel = RC ? &rc_del : nullptr;
   uint32_t* const rhalt = RC ? &rc_halt : nullptr;
+  // REGS: the per-cluster trip count (the packing key), the client batch's start and the per-lane
+  // deferred-draw bit in registers instead of LDS where registers are to spare (N >= 7, and the
+  // Spec-Raft N = 6 kernel): LDS round trips off every trip's chain (C4-N9 -9 %)
+  constexpr bool REGS = !LITE && !STORM && N >= RS_REGS_MIN_N && (SPEC || N >= 7);
+  uint32_t trips_r = 0, dpend_r = 0, cb_r = 0;   // cb_r: the client batch's start (cq_base)
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -554,7 +563,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       n.votes = mk & 0xFFFF; n.keys = mk >> 16 | ((fl >> 14) & 1);
       n.term = hp[HF_TERM * N]; n.commit = hp[HF_COMMIT * N]; n.len = hp[HF_LEN * N];
       n.deadline = hp[HF_DEADLINE * N];
-      if (!SPEC) dpend[lane] = (fl & FL_DRAW) ? 1u : 0u;   // a deferred draw carried over
+      if (!SPEC) {                                        // a deferred draw carried over
+        if constexpr (REGS) dpend_r = (fl & FL_DRAW) ? 1u : 0u;
+        else dpend[lane] = (fl & FL_DRAW) ? 1u : 0u;
+      }
       n.rq.h = qm & 15; n.rq.c = (qm >> 4) & 31; n.rs.h = (qm >> 9) & 15; n.rs.c = (qm >> 13) & 31;
       n.rq.arr = hp[HF_REQ_ARR * N]; n.rs.arr = hp[HF_RES_ARR * N];
       n.rq.tail = hp[HF_REQ_TAIL * N]; n.rs.tail = hp[HF_RES_TAIL * N];
@@ -707,7 +719,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       if constexpr (!LITE) {
         const uint32_t cw = (uint32_t)bl0 / N;
         const bool want = active && cnext < tend;
-        if (__ballot(want && t == cnext && ccount - cq_base[cw] >= (uint32_t)N)) {
+        if (__ballot(want && t == cnext && ccount - (REGS ? cb_r : cq_base[cw]) >= (uint32_t)N)) {
           RS_PX(wl_px0);
           const uint4 d = philox(g, P_CLIENT << 8, ccount + (uint32_t)k0, 0, S.key0, S.key1);
           // (the fields by scalar loads here: kargs)
@@ -729,13 +741,15 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             const uint64_t oi = P ? (uint64_t)q * db.d + (cnext - q * P) : cnext;   // on_index
             cq_nxt[lane] = on_tick(oi + x, P, db);
             cq_tgt[lane] = (uint8_t)(1 + __umulhi(d.y, N));
-            if (k0 == 0) cq_base[cw] = ccount;
+            if constexpr (REGS) cb_r = ccount;          // (every lane of the cluster)
+            else if (k0 == 0) cq_base[cw] = ccount;
           }
         }
       }
     };
     if constexpr (!LITE) {
-      if (active && k0 == 0) cq_base[cs] = ccount - N;    // empty
+      if constexpr (REGS) cb_r = ccount - N;              // empty
+      else if (active && k0 == 0) cq_base[cs] = ccount - N;
     }
     // A non-leader's re-armed timer (D4: t + el_base + the EVENT draw's word 1) is only compared
     // with ticks at or past t + el_base, so its draw is deferred (dpend) unless the event drew
@@ -748,7 +762,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       t = t < tend ? t : tend;
       const bool on = active && t < tend;     // the cluster has a tick to run in this trip
       if (!__ballot(on)) break;
-      if (!LITE && k0 == 0 && kargs()->client_ppm) tripsL[(uint32_t)bl0 / N] += on;
+      if constexpr (REGS) trips_r += on;        // (cluster-uniform; used with client traffic)
+      else if (!LITE && k0 == 0 && kargs()->client_ppm) tripsL[(uint32_t)bl0 / N] += on;
   #ifdef RS_WAVELOG
       RS_PHASE(8);
   #endif
@@ -788,7 +803,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           if constexpr (RC) rc_inj += (uint32_t)__popcll(heads);        // (wave-uniform)
           else if (lane == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, (uint32_t)__popcll(heads));
           if (cinj) {
-            const uint32_t s = (uint32_t)bl + (ccount - cq_base[cw]);
+            const uint32_t s = (uint32_t)bl + (ccount - (REGS ? cb_r : cq_base[cw]));
             if (cq_tgt[s] == id) {
               inj = true;
               injv = cq_val[s];
@@ -836,7 +851,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // The next timeout of a non-leader (core.clj:174) takes the tick's draw when there is one,
       // else its draw is deferred (leaders' events need none).
       uint4 w = make_uint4(0, 0, 0, 0);
-      const bool tdraw = !SPEC && !STORM && live && dpend[lane] && !req_ok && !res_ok &&
+      const bool tdraw = !SPEC && !STORM && live && (REGS ? dpend_r : dpend[lane]) && !req_ok && !res_ok &&
                          n.deadline <= t;
       bool have_w = (req_ok && res_ok) ||
                     (!LITE && req_ok && n.role != RAFT_LEADER && n.lid == 0);
@@ -846,7 +861,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       }
       if (tdraw) {
         n.deadline += __umulhi(w.y, kargs()->el_span);
-        dpend[lane] = 0;
+        if constexpr (REGS) dpend_r = 0;
+        else dpend[lane] = 0;
       }
       if (live && (req_ok || res_ok || t >= n.deadline)) {
         int which = -1;
@@ -1111,7 +1127,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           if (n.role == RAFT_LEADER) {
             if (!SPEC || ev == 7 || elected) {
               n.deadline = t + kargs()->hb;
-              dpend[lane] = 0;
+              if constexpr (REGS) dpend_r = 0;
+              else dpend[lane] = 0;
             }
           } else if (!SPEC || ev == 6 || rearm || was_leader) {
             // Spec-Raft re-arms on few events (SIM_SPEC §8): drawn at once there
@@ -1119,7 +1136,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             const bool defer = !SPEC && !have_w;
             KDevSim* const K = kargs();
             n.deadline = t + K->el_base + (defer ? 0u : __umulhi(w.y, K->el_span));
-            if (!SPEC) dpend[lane] = defer;                    // the draw is deferred
+            if (!SPEC) {                                       // the draw is deferred
+              if constexpr (REGS) dpend_r = defer;
+              else dpend[lane] = defer;
+            }
             have_w = have_w || SPEC;
           }
           n.trace = trace_event(n.trace, t, ev, tsrc, tterm, n.role, n.term, 0);
@@ -1724,7 +1744,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
 
     // ---------------------------------------------------------------- write back
     // a deferred draw stays owed in the stored state (FL_DRAW, device.hpp)
-    const uint32_t owed = !SPEC && active && dpend[lane] ? FL_DRAW : 0u;
+    const uint32_t owed = !SPEC && active && (REGS ? dpend_r : dpend[lane]) ? FL_DRAW : 0u;
     if (!SPEC) dpend[lane] = 0;
     KDevSim* const KW = kargs();
     if (KW->shist) {
@@ -1745,7 +1765,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       const uint32_t key = !head ? INF
                            : KW->client_ppm
                                ? (dead ? SCHED_BUCKETS - 1
-                                       : SCHED_BUCKETS - 2 - min(tripsL[cs], SCHED_BUCKETS - 2))
+                                       : SCHED_BUCKETS - 2 -
+                                             min(REGS ? trips_r : tripsL[cs], SCHED_BUCKETS - 2))
                                : sched_bucket(cm, tend);
       if (head) KW->skey[c] = key;
       // a packed wave's clusters usually share their next key: one histogram atomic for the wave
