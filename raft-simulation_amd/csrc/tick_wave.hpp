@@ -27,6 +27,9 @@ namespace rs {
 #ifndef RS_REGS_MIN_N
 #define RS_REGS_MIN_N 6
 #endif
+#ifndef RS_KA_HOIST
+#define RS_KA_HOIST 1
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -506,6 +509,16 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   // Spec-Raft N = 6 kernel): LDS round trips off every trip's chain (C4-N9 -9 %)
   constexpr bool REGS = !LITE && !STORM && N >= RS_REGS_MIN_N && (SPEC || N >= 7);
   uint32_t trips_r = 0, dpend_r = 0, cb_r = 0;   // cb_r: the client batch's start (cq_base)
+  // (REGS kernels also read the kernel-argument fields a trip's common handlers use once, here,
+  // instead of a scalar load and its wait at every use)
+  uint32_t ka_el_base = 0, ka_el_span = 0, ka_hb = 0, ka_L = 0, ka_redir = 0;
+  bool ka_fixd = false;
+  if constexpr (REGS && RS_KA_HOIST) {
+    KDevSim* const K0 = kargs();
+    ka_el_base = K0->el_base; ka_el_span = K0->el_span; ka_hb = K0->hb; ka_L = K0->L;
+    ka_redir = K0->client_redirects; ka_fixd = K0->dmin == K0->dmax;
+  }
+  constexpr bool KAH = REGS && RS_KA_HOIST;
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -857,10 +870,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                     (!LITE && req_ok && n.role != RAFT_LEADER && n.lid == 0);
       if (have_w || tdraw) {
         RS_PX(wl_px2);
-        w = event_draw(sg, id, tdraw ? n.deadline - kargs()->el_base : t, S);
+        w = event_draw(sg, id, tdraw ? n.deadline - (KAH ? ka_el_base : kargs()->el_base) : t, S);
       }
       if (tdraw) {
-        n.deadline += __umulhi(w.y, kargs()->el_span);
+        n.deadline += __umulhi(w.y, KAH ? ka_el_span : kargs()->el_span);
         if constexpr (REGS) dpend_r = 0;
         else dpend[lane] = 0;
       }
@@ -1014,7 +1027,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 }
                 n.seq = 1;
               } else {
-                if (n.len + pcnt > kargs()->L) {
+                if (n.len + pcnt > (KAH ? ka_L : kargs()->L)) {
                   fault = RAFT_FAULT_OVERFLOW;
                   break;
                 }
@@ -1048,7 +1061,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
                 emit = 4;
                 break;
               }
-              if (n.len + 1 > kargs()->L) {
+              if (n.len + 1 > (KAH ? ka_L : kargs()->L)) {
                 fault = RAFT_FAULT_OVERFLOW;
                 break;
               }
@@ -1126,7 +1139,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // (D4); Spec-Raft keeps Raft's timers (SIM_SPEC §8)
           if (n.role == RAFT_LEADER) {
             if (!SPEC || ev == 7 || elected) {
-              n.deadline = t + kargs()->hb;
+              n.deadline = t + (KAH ? ka_hb : kargs()->hb);
               if constexpr (REGS) dpend_r = 0;
               else dpend[lane] = 0;
             }
@@ -1135,7 +1148,8 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             if (SPEC && !have_w) w = event_draw(sg, id, t, S);
             const bool defer = !SPEC && !have_w;
             KDevSim* const K = kargs();
-            n.deadline = t + K->el_base + (defer ? 0u : __umulhi(w.y, K->el_span));
+            n.deadline = t + (KAH ? ka_el_base : K->el_base) +
+                         (defer ? 0u : __umulhi(w.y, KAH ? ka_el_span : K->el_span));
             if (!SPEC) {                                       // the draw is deferred
               if constexpr (REGS) dpend_r = defer;
               else dpend[lane] = defer;
@@ -1179,7 +1193,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // (a stepped-down leader keeps its :leader-id) goes through the sender record alone.
           if (!LITE && emit == 4) {
             emit = 0;
-            if (mb >= kargs()->client_redirects) {
+            if (mb >= (KAH ? ka_redir : kargs()->client_redirects)) {
               lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
             } else {
               uint32_t dst = n.lid;
@@ -1521,7 +1535,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           // scratch, and their payloads are short)
           KDevSim* const KG = kargs();
           if constexpr (N >= 6) {
-            if (KG->dmin == KG->dmax) log_match(std::true_type{});
+            if (KAH ? ka_fixd : KG->dmin == KG->dmax) log_match(std::true_type{});
             else log_match(std::false_type{});
           } else {
             log_match(std::false_type{});
