@@ -30,6 +30,9 @@ namespace rs {
 #ifndef RS_KA_HOIST
 #define RS_KA_HOIST 1
 #endif
+#ifndef RS_SHFL_GUARD
+#define RS_SHFL_GUARD 1
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -1364,7 +1367,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       const uint32_t m = pkind == PLAN_PAYLOAD ? ppcnt : (pkind == PLAN_ENTRY ? 1u : 0u);
       const int appended_at = m ? (int)(n.len - m) : -1;
       if (!STORM && __ballot(m || papplied || (TRACE && tr_cnt))) {
-        const uint32_t sfront = __shfl(n.front, bl + (int)psrc - 1);
+        // (the sender's frontier matters to payload appends only: no shuffle on entry-only trips)
+        const uint32_t sfront = !RS_SHFL_GUARD || __ballot(m && pkind == PLAN_PAYLOAD)
+                                    ? (uint32_t)__shfl(n.front, bl + (int)psrc - 1) : 0u;
         if (m) {
           const uint32_t pold_len = n.len - m;
           // physical slots advance with a wrap instead of a per-entry modulo
@@ -1541,8 +1546,10 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
             log_match(std::false_type{});
           }
           uint32_t fa = 0;
+          if (!RS_SHFL_GUARD || __ballot(found != 0)) {       // (a conflict is rare)
   #pragma unroll
-          for (int s = 0; s < N; ++s) fa |= (uint32_t)__shfl((int)found, bl + s);
+            for (int s = 0; s < N; ++s) fa |= (uint32_t)__shfl((int)found, bl + s);
+          }
           const bool bad = active && ((fa >> k) & 1);
           if (bad) violation(lctr, RAFT_CTR_VIOL_LOG, t);
         }
