@@ -503,14 +503,14 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
   // added to the wave's LDS counters once at the end: N >= 7 (three waves per SIMD anyway; C4
   // -5 %) and Spec-Raft (C3-spec -3 %); the faithful N <= 5 kernel measured the same either way,
   // and the faithful N = 6 kernel keeps its four waves per SIMD without them
-  constexpr bool RC = !LITE && !STORM && (SPEC || (N >= RS_RC_MIN_N && N >= 7));
+  constexpr bool RC = !LITE && ((N >= RS_RC_MIN_N && N >= 7) || (SPEC && !STORM));
   uint32_t rc_cs = 0, rc_red = 0, rc_del = 0, rc_app = 0, rc_inj = 0, rc_halt = 0;
   uint32_t* const rdel = RC ? &rc_del : nullptr;
   uint32_t* const rhalt = RC ? &rc_halt : nullptr;
   // REGS: the per-cluster trip count (the packing key), the client batch's start and the per-lane
   // deferred-draw bit in registers instead of LDS where registers are to spare (N >= 7, and the
   // Spec-Raft N = 6 kernel): LDS round trips off every trip's chain (C4-N9 -9 %)
-  constexpr bool REGS = !LITE && !STORM && N >= RS_REGS_MIN_N && (SPEC || N >= 7);
+  constexpr bool REGS = !LITE && N >= RS_REGS_MIN_N && (N >= 7 || (SPEC && !STORM));
   uint32_t trips_r = 0, dpend_r = 0, cb_r = 0;   // cb_r: the client batch's start (cq_base)
   // (REGS kernels also read the kernel-argument fields a trip's common handlers use once, here,
   // instead of a scalar load and its wait at every use)
