@@ -33,6 +33,21 @@ namespace rs {
 #ifndef RS_SHFL_GUARD
 #define RS_SHFL_GUARD 1
 #endif
+#ifndef RS_BURST
+#define RS_BURST 1
+#endif
+#ifndef RS_BURST_KO_CMP  // timing-only knock-out of the burst engine's log-matching loads (wrong results)
+#define RS_BURST_KO_CMP 0
+#endif
+#ifndef RS_BURST_MIN      // the shortest engine run worth an entry (ticks)
+#define RS_BURST_MIN 16
+#endif
+#ifndef RS_BURST_PRE      // evaluate the engine's entry only on trips with an injection or a queued leader
+#define RS_BURST_PRE 0
+#endif
+#ifndef RS_BURST_DIAG   // timing-only diagnostic builds: engine ticks, entries, yields and trips in
+#define RS_BURST_DIAG 0 // four counters C4 never uses (wrong counters): never set in the product
+#endif
 
 // knock-out switches of timing-only diagnostic builds (wrong results): never set in the product
 #ifndef RS_KO_P4
@@ -522,6 +537,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     ka_redir = K0->client_redirects; ka_fixd = K0->dmin == K0->dmax;
   }
   constexpr bool KAH = REGS && RS_KA_HOIST;
+  // BURST: the faithful N >= 7 kernels run a cluster's client burst under a stable leader in a
+  // lane loop of its own (the burst engine in the tick loop below)
+  constexpr bool BURST = RS_BURST && KAH && !SPEC && !STORM && !TRACE && !LITE && !CATCH && N >= 7;
   // the wave's cells, counters, leader rows and per-lane / per-cluster words
   uint32_t* cells = smem;
   uint32_t* lctr = cells + cell_words<N>();
@@ -773,11 +791,189 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // also serves as the cluster's next event; when a tick at or past it comes with no message
     // ready (a message wins, D3, and in the faithful model its event re-arms the timer anyway) the
     // draw is made in P1 and the timeout decided on the exact deadline, else at the write-back.
+    // the burst engine's launch-wide gate: client traffic, and ticks that fit its 28-bit arrivals
+    constexpr uint32_t BAM = (1u << 28) - 1;
+    const bool bclient = BURST && kargs()->client_ppm != 0 && tend <= BAM;
     for (;;) {
       uint32_t t = max(tnext, next_event());
       t = t < tend ? t : tend;
+      // ------------------------------------------------------------------ burst engine (BURST)
+      // A client burst under a stable leader is a chain of events that each touch one node: a
+      // client-set injected at a follower is redirected to the :leader-id (server.clj:62-63)
+      // and reaches the leader at t + 1 (D15); the leader takes one client-set per tick and
+      // appends it (core.clj:157-160), re-arming its timer every time, so no heartbeat fires and
+      // no network message exists. A cluster whose state at its next event tick is such a state
+      // -- one live leader L with empty RES and REQ queues, its log at its arena frontier and no
+      // owed draw; every other live node a non-leader with :leader-id L, empty queues and a
+      // deadline ahead; halted nodes anywhere -- runs its ticks here, its N lanes in step, one
+      // loop trip per event tick, instead of a trip of the tick loop with its five phases. Every
+      // lane tracks the leader's ring (at most two client-sets: one arrives per tick, one leaves),
+      // its log length and deadline, so the target of each injection decides each lane's work
+      // without a shuffle. The loop stops before the first tick with anything else -- a
+      // follower's deadline (its deferred draw, a timeout), the leader's heartbeat, the leader's
+      // OVERFLOW, a full one-slot inbox, the launch's end -- and the tick loop resumes the cluster
+      // there (all ticks before it are done: `tnext`). Per tick and node it does what the phases
+      // do: P0's injection (batch, counters, to-halted), P1's handlers (trace hash, re-arm, the
+      // deferred draw of a follower, redirect or abandon), P2's delivery to the leader, P3's entry
+      // append and P4's log matching of the new entry against every other node's log.
+      if constexpr (BURST) {
+        if (bclient && (!RS_BURST_PRE ||
+                        __ballot(active && t < tend &&
+                                 (t == cnext || (n.role == RAFT_LEADER && n.rq.c == 1))))) {
+          const bool live0 = active && !n.fault;
+          const uint32_t lmask = (uint32_t)(__ballot(live0) >> bl0) & cmask;
+          const uint32_t ldm = (uint32_t)(__ballot(live0 && n.role == RAFT_LEADER) >> bl0) & cmask;
+          const int Lk = ldm ? (int)__builtin_ctz(ldm) : 0;
+          const bool isL = k0 == Lk;
+          const bool lok = !live0 ||
+                           (isL ? (n.rq.c <= 1 && n.rs.c == 0 && n.base + n.len == n.front && !dpend_r)
+                                : (n.lid == (uint32_t)Lk + 1 && n.rq.c == 0 && n.rs.c == 0 &&
+                                   n.deadline > t));
+          bool bok = active && t < tend && __popc(ldm) == 1 && !cluster_any(!lok);
+          const bool Lq = cluster_any(isL && n.rq.c != 0);    // (one queued message at most)
+          bok = bok && (t == cnext || Lq);
+          // Clusters that stay with the tick loop bound the run: an engine cluster runs no tick
+          // past the latest next-event tick among them (after its first), so a burst's engine ticks
+          // spread over the trips the other clusters take anyway instead of following them; the
+          // run then yields (the tick loop takes its next tick, and the next trip re-enters). A
+          // cluster that could run fewer than BURST_MIN ticks that way stays with this trip (an
+          // entry costs about a trip).
+          const bool oth = active && !bok && t < tend;
+          const uint32_t tlim = __ballot(oth) ? ~wave_min(oth ? ~t : ~0u) : INF;
+          constexpr uint32_t BURST_MIN = RS_BURST_MIN;
+          bok = bok && (tlim == INF || tlim >= t + BURST_MIN);
+          if (__ballot(bok)) {
+            // the leader's queued message enters with the cluster if it is a client-set due by t
+            uint4 lm0 = make_uint4(0, 0, 0, 0), lm1 = make_uint4(0, 0, 0, 0);
+            if (bok && Lq) {
+              const uint32_t* qb = qslots(S, c * N + (uint32_t)Lk, 0) +
+                                   (uint32_t)__shfl((int)n.rq.h, bl0 + Lk) * qstride(S, 0);
+              lm0 = *reinterpret_cast<const uint4*>(qb);
+              lm1 = *reinterpret_cast<const uint4*>(qb + 4);
+              bok = lm0.y == RAFT_MSG_CLIENT_SET && lm0.z == 0 && lm0.x <= t && lm1.x < 16 &&
+                    !lm1.y && !lm1.z && !lm1.w;
+            }
+            if (bok) {                                   // whole clusters: cluster-uniform below
+              const uint32_t Lid = (uint32_t)Lk + 1;
+              const uint32_t Llen0 = (uint32_t)__shfl((int)n.len, bl0 + Lk);
+              const uint32_t Lterm = (uint32_t)__shfl((int)n.term, bl0 + Lk);
+              uint32_t Llen = Llen0, Ldl = (uint32_t)__shfl((int)n.deadline, bl0 + Lk);
+              // the live followers' earliest deadline, kept as a lower bound (an event re-arms its
+              // follower to tc + el_base) and recomputed when a tick reaches it; the longest other
+              // log (the checker compares only positions it reaches)
+              const bool fol = live0 && !isL;
+              uint32_t fmin = cluster_min(fol ? n.deadline : INF);
+              const uint32_t omax = ~cluster_min(isL ? ~0u : ~n.len);
+              // the leader's REQ ring: at most one client-set (arrival | hops << 28, value) between
+              // ticks -- a tick adds at most one and the leader takes one whenever it holds any
+              uint32_t rc = Lq ? 1u : 0u, qa0 = lm0.x | lm1.x << 28, qv0 = lm0.w, binj = 0, eticks = 0;
+              uint2* const own = arena_of(S, gi);
+              // the lane's arena slot of log position Llen, and its entry there (the checker's next
+              // comparison, loaded a tick ahead of its use)
+              uint32_t as = (n.base + Llen0) % A;
+              uint2 pre = make_uint2(0, 0);
+              if (!RS_BURST_KO_CMP && !isL && n.len > Llen0) pre = own[as];
+              uint32_t tc = t;
+              for (;;) {
+                if (tc >= tend || (tc > tlim && tc != t)) break;
+                if (tc >= fmin) {                        // a follower's deadline may be due
+                  fmin = cluster_min(fol ? n.deadline : INF);
+                  if (tc >= fmin) break;
+                }
+                const bool injn = tc == cnext;
+                uint32_t tgt = 0, val = 0, nxt = 0;
+                if (injn) {
+                  refill_batch(tc);
+                  const uint32_t s = (uint32_t)bl0 + (ccount - cb_r);
+                  tgt = cq_tgt[s];
+                  val = cq_val[s];
+                  nxt = cq_nxt[s];
+                }
+                const bool toL = injn && tgt == Lid;
+                const bool evL = rc || toL;
+                if ((!evL && Ldl <= tc) || (evL && Llen >= ka_L) || rc >= S.Q) break;
+                ++eticks;
+                if (RS_BURST_DIAG && k0 == 0) lctr_add(lctr, RAFT_CTR_DROPPED, 1);
+                // a live follower's event: redirect-client (server.clj:62-63), or abandon
+                const bool tof = injn && !toL && ((lmask >> (tgt - 1)) & 1);
+                const bool red = tof && ka_redir != 0;
+                const uint32_t pv = rc ? qv0 : val;      // the client-set the leader takes
+                // the ring after the tick: the injection behind a queued one, or a redirect
+                // arriving at tc + 1 (P2), else empty
+                const bool keep = rc && toL;
+                qa0 = keep ? tc : (tc + 1) | 1u << 28;
+                qv0 = val;
+                rc = keep || red ? 1u : 0u;
+                if (injn) {
+                  ccount += 1;
+                  cnext = nxt;
+                  binj += k0 == 0 ? 1u : 0u;
+                }
+                // one handler per lane: the leader's append (client-set-handler 157-160) or the
+                // target follower's redirect; every event re-arms the timer (a follower's draw is
+                // deferred: no EVENT draw at a known :leader-id)
+                const bool me = isL ? evL : tof && k0 + 1 == (int)tgt;
+                if (me) {
+                  n.trace = trace_event(n.trace, tc, RAFT_MSG_CLIENT_SET, 0, 0, n.role, n.term, 0);
+                  ++rc_cs;
+                  rc_app += isL ? 1u : 0u;
+                  if (!isL) {
+                    n.deadline = tc + ka_el_base;
+                    dpend_r = 1;
+                  }
+                }
+                if (tof) fmin = min(fmin, tc + ka_el_base);   // (every lane of the cluster)
+                // deliveries (the injection taken or queued, the redirect into the leader's ring),
+                // redirects, abandoned client-sets, injections into halted nodes
+                rc_del += isL ? (toL ? 1u : 0u) + (red ? 1u : 0u) : (me ? 1u : 0u);
+                if (!isL && me) {
+                  if (red) ++rc_red;
+                  else lctr_add(lctr, RAFT_CTR_CLIENT_ABANDONED, 1);
+                }
+                rc_halt += injn && !toL && !tof && k0 + 1 == (int)tgt ? 1u : 0u;
+                if (evL) {
+                  // P3 / P4: the entry (Lterm, pv) at position p, and log matching against every
+                  // other node's log that reaches p
+                  const uint32_t p = Llen;
+                  Llen = p + 1;
+                  Ldl = tc + ka_hb;
+                  if (isL) own[as] = make_uint2(Lterm, pv);
+                  const bool conf = !isL && n.len > p && pre.x == Lterm && pre.y != pv;
+                  as = as + 1 == A ? 0u : as + 1;
+                  if (!RS_BURST_KO_CMP && !isL && n.len > p + 1) pre = own[as];
+                  if (p < omax && cluster_any(conf) && isL) violation(lctr, RAFT_CTR_VIOL_LOG, tc);
+                }
+                tc = max(tc + 1, min(min(cnext, rc ? tc + 1 : INF), min(min(Ldl, fmin), tend)));
+              }
+              if (isL) {                                 // the leader's words, its ring as the tick loop keeps it
+                if (Llen != Llen0) {
+                  n.front += Llen - Llen0; n.len = Llen; n.seq = 0; n.deadline = Ldl;
+                }
+                if (rc) {
+                  uint32_t* const qb = qslots(S, gi, 0);
+                  *reinterpret_cast<uint4*>(qb) = make_uint4(qa0 & BAM, RAFT_MSG_CLIENT_SET, 0, qv0);
+                  *reinterpret_cast<uint4*>(qb + 4) = make_uint4(qa0 >> 28, 0, 0, 0);
+                }
+                n.rq.h = 0; n.rq.c = rc; n.rq.arr = rc ? qa0 & BAM : INF; n.rq.tail = rc ? qa0 & BAM : 0u;
+              }
+              if (k0 == 0) lctr_add(lctr, RAFT_CTR_CLIENT_INJECTED, binj);
+              // the packing key counts an engine tick as an eighth of a trip: clusters the tick loop
+              // keeps busy through a burst are then packed together, ahead of the engine's
+              trips_r += eticks >> 3;
+              if (RS_BURST_DIAG && k0 == 0) {
+                lctr_add(lctr, RAFT_CTR_DUPLICATED, 1);
+                lctr_add(lctr, RAFT_CTR_PARTITIONED, tc > tlim && tc < tend ? 1u : 0u);
+              }
+              tnext = tc;
+            }
+            t = max(tnext, next_event());
+            t = t < tend ? t : tend;
+          }
+        }
+      }
       const bool on = active && t < tend;     // the cluster has a tick to run in this trip
       if (!__ballot(on)) break;
+      if (BURST && RS_BURST_DIAG && on && k0 == 0) lctr_add(lctr, RAFT_CTR_PAYLOAD_EVICTED, 1);
       if constexpr (REGS) trips_r += on;        // (cluster-uniform; used with client traffic)
       else if (!LITE && k0 == 0 && kargs()->client_ppm) tripsL[(uint32_t)bl0 / N] += on;
   #ifdef RS_WAVELOG

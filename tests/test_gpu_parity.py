@@ -74,6 +74,18 @@ CASES = {
     # BASELINE config 4: 7 and 9 nodes, 4096-entry logs, bursts that build 1000+-entry batches
     "c4_n7_bursts": dict(n_clusters=512, nodes=7, seed=3, commit_stream_cap=256, **C4_BURSTS),
     "c4_n9_bursts": dict(n_clusters=256, nodes=9, seed=5, dup_ppm=20000, dmax=8, **C4_BURSTS),
+    # the N >= 7 burst engine's edges (tick_wave.hpp BURST): no redirect hops (abandoned
+    # client-sets) with one-slot inboxes; follower timers and heartbeats that fall inside bursts;
+    # launches that split bursts at odd ticks
+    "burst_edges_n7": dict(n_clusters=512, nodes=7, seed=91, client_ppm=500000, client_period=4096,
+                           client_burst=1024, client_redirects=0, inbox_cap=1, log_cap=700, hb=300,
+                           el_base=500, el_span=500),
+    "burst_timers_n9": dict(n_clusters=512, nodes=9, seed=93, client_ppm=300000, client_period=2048,
+                            client_burst=512, client_redirects=1, inbox_cap=2, log_cap=2000, hb=40,
+                            el_base=60, el_span=40),
+    "burst_launches_n8": dict(n_clusters=512, nodes=8, seed=95, client_ppm=500000,
+                              client_period=1024, client_burst=256, client_redirects=4,
+                              ticks_per_launch=37, log_cap=1500),
     # config 3 / 5 shapes with the bursty, redirect-following client
     "c3_bursts": dict(n_clusters=2048, nodes=5, seed=1, client_ppm=80000, log_cap=256,
                       **BURSTS, **FAULTS),
