@@ -42,6 +42,9 @@ namespace rs {
 #ifndef RS_BURST_MIN      // the shortest engine run worth an entry (ticks)
 #define RS_BURST_MIN 16
 #endif
+#ifndef RS_BURST_SKIP     // trips a wave skips the engine's entry check after one that found no entry
+#define RS_BURST_SKIP 8
+#endif
 #ifndef RS_BURST_PRE      // evaluate the engine's entry only on trips with an injection or a queued leader
 #define RS_BURST_PRE 0
 #endif
@@ -794,6 +797,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
     // the burst engine's launch-wide gate: client traffic, and ticks that fit its 28-bit arrivals
     constexpr uint32_t BAM = (1u << 28) - 1;
     const bool bclient = BURST && kargs()->client_ppm != 0 && tend <= BAM;
+    // (wave-uniform) trips left before the entry check runs again: a check that finds no cluster
+    // to enter costs about a tenth of a trip, and states change slowly against trips
+    uint32_t bskip = 0;
     for (;;) {
       uint32_t t = max(tnext, next_event());
       t = t < tend ? t : tend;
@@ -817,7 +823,9 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
       // deferred draw of a follower, redirect or abandon), P2's delivery to the leader, P3's entry
       // append and P4's log matching of the new entry against every other node's log.
       if constexpr (BURST) {
-        if (bclient && (!RS_BURST_PRE ||
+        if (bskip) {
+          --bskip;
+        } else if (bclient && (!RS_BURST_PRE ||
                         __ballot(active && t < tend &&
                                  (t == cnext || (n.role == RAFT_LEADER && n.rq.c == 1))))) {
           const bool live0 = active && !n.fault;
@@ -842,6 +850,7 @@ __device__ __forceinline__ void tick_wave(const DevSim& S, uint32_t t0, uint32_t
           const uint32_t tlim = __ballot(oth) ? ~wave_min(oth ? ~t : ~0u) : INF;
           constexpr uint32_t BURST_MIN = RS_BURST_MIN;
           bok = bok && (tlim == INF || tlim >= t + BURST_MIN);
+          if (!__ballot(bok)) bskip = RS_BURST_SKIP;
           if (__ballot(bok)) {
             // the leader's queued message enters with the cluster if it is a client-set due by t
             uint4 lm0 = make_uint4(0, 0, 0, 0), lm1 = make_uint4(0, 0, 0, 0);
